@@ -1,0 +1,165 @@
+/*
+ * p2pmg.h — C ABI of libp2pmg.so, the MI355X (gfx950) batched simulator/trainer for the
+ * P2PMicrogrid hot path: per-timestep community rollout + tabular Q-learning update,
+ * vectorised over S independent community scenarios x N agents.
+ *
+ * Reference interfaces replaced (paths relative to /root/reference/microgrid):
+ *   p2pmg_run_episode(TRAIN)   CommunityMicrogrid.train_episode          community.py:149-182
+ *                              (+ _run :67-93, _assign_powers :45-54, _compute_costs :56-65,
+ *                               RLAgent.__call__/_divide_power/get_reward agent.py:172-232,
+ *                               QAgent._act/train agent.py:271-298, QActor rl.py:89-129,
+ *                               HPHeating.step / temperature_simulation heating.py:37-56,138-143)
+ *   p2pmg_run_episode(GREEDY)  CommunityMicrogrid.run                    community.py:95-123
+ *                              (QAgent.take_decision agent.py:277-289, QActor.greedy_action rl.py:113-117)
+ *   p2pmg_set_env              env.setup(dataset) / GridAgent prices     environment.py:26-45, agent.py:59-67
+ *   p2pmg_set_profiles         agent load / Prosumer PV streams          agent.py:78-79,100-103, production.py:23-41
+ *   p2pmg_set_agent_params     get_community max_in                      community.py:216-227
+ *   p2pmg_set_temperatures     HPHeating.__init__/reset T0               heating.py:101-104,145-152
+ *   p2pmg_get_q / p2pmg_set_q  QActor.q_table / set_qtable               rl.py:76-81 (layout (20,20,20,20,3))
+ *   p2pmg_rc_step              heating.temperature_simulation (batched)  heating.py:37-56
+ *   p2pmg_state_indices        QActor._get_state_indices (batched)       rl.py:89-95
+ *   p2pmg_replay_decode        np.random rand()/choice(3) consumption    rl.py:100-111 (legacy MT19937)
+ *
+ * Conventions: every function returns an int status (P2PMG_OK = 0); no C++ exception crosses
+ * the ABI; a per-context error string is available from p2pmg_last_error().  A context owns
+ * one device, one HIP stream and every device buffer; host pointers are borrowed for the
+ * duration of the call only (copied in/out).  Calls are stream-ordered; p2pmg_sync() (or any
+ * p2pmg_get_*) completes outstanding work before host reads.  A context is not thread-safe:
+ * use one process per GPU for multi-GPU (scenarios are sharded across ranks).
+ */
+#ifndef P2PMG_H
+#define P2PMG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define P2PMG_ABI_VERSION 1
+
+typedef struct p2pmg_ctx p2pmg_ctx;
+
+/* status codes */
+#define P2PMG_OK 0
+#define P2PMG_E_INVALID 1     /* bad argument / shape */
+#define P2PMG_E_HIP 2         /* HIP runtime error (message in p2pmg_last_error) */
+#define P2PMG_E_NOMEM 3       /* device allocation failed */
+#define P2PMG_E_STATE 4       /* missing prerequisite (e.g. profiles not set) */
+#define P2PMG_E_UNSUPPORTED 5 /* configuration not compiled in (e.g. N > 16) */
+
+/* Q-table element type: f64 = the reference's np.zeros table (rl.py:73), bit-exact;
+ * f32 = throughput mode (TD update in f32, held to 1e-5 relative). */
+#define P2PMG_Q_F64 0
+#define P2PMG_Q_F32 1
+
+#define P2PMG_MODE_TRAIN 0  /* train_episode: epsilon-greedy + TD update */
+#define P2PMG_MODE_GREEDY 1 /* run(): greedy actions, no update, no RNG */
+
+#define P2PMG_RNG_REPLAY 0 /* exploration codes supplied by the host (reference stream) */
+#define P2PMG_RNG_PHILOX 1 /* counter-keyed Philox4x32-10 on (seed, episode, agent, t, round) */
+
+/* per-step records (bit mask for p2pmg_episode_args.record and p2pmg_get_record) */
+#define P2PMG_REC_REWARD 1   /* f32 [T][A] reward (agent.py:225-232) */
+#define P2PMG_REC_COST 2     /* f32 [T][A] cost   (community.py:56-65) */
+#define P2PMG_REC_GRID 4     /* f32 [T][A] p_grid (community.py:51) */
+#define P2PMG_REC_P2P 8      /* f32 [T][A] p_p2p  (community.py:52) */
+#define P2PMG_REC_TEMP 16    /* f32 [T][A] T_in before the step's RC update (heating.py:139) */
+#define P2PMG_REC_ACTION 32  /* u8  [T][R+1][A] action index (decisions, community.py:88-89) */
+#define P2PMG_REC_INDEX 64   /* i32 [T][R+1][A] packed state index it | iT<<8 | ib<<16 | ip<<24 */
+
+#define P2PMG_GREEDY 255 /* replay code: no exploration in this (t, round, agent) */
+
+typedef struct p2pmg_config {
+  int32_t n_scenarios;      /* S */
+  int32_t n_agents;         /* N agents per scenario (1..16) */
+  int32_t rounds;           /* R: negotiation runs R+1 rounds (community.py:75) */
+  int32_t horizon;          /* T timesteps per episode */
+  int32_t q_dtype;          /* P2PMG_Q_F64 | P2PMG_Q_F32 */
+  int32_t n_time_states;    /* 20 (agent.py:258-261) */
+  int32_t n_temp_states;    /* 20 */
+  int32_t n_balance_states; /* 20 */
+  int32_t n_p2p_states;     /* 20 */
+  int32_t n_actions;        /* 3 (<= 4) */
+  double alpha;             /* 1e-5 (rl.py:60) */
+  double gamma;             /* 0.9  (rl.py:59) */
+  float hp_levels[4];       /* f32(level * max_power) = {0, 1500, 3000} W (agent.py:268, heating.py:124) */
+  float setpoint;           /* 21 (community.py:226) */
+  float temp_margin;        /* 1  (heating.py:90) */
+  float lower_bound;        /* 20 (heating.py:93) */
+  float upper_bound;        /* 22 */
+  /* RC model, f32 casts of the Python doubles (heating.py:23-56) */
+  float inv_ci, inv_cm, inv_ri, inv_re, inv_rvent;
+  float one_minus_frad; /* f32(1 - f_rad) */
+  float frad;           /* f32(f_rad) */
+  float solar_gain;     /* f32(gA * solar_rad) = 0 */
+  float hp_cop;         /* f32(3.0) */
+  float seconds_per_minute; /* 60 */
+  float time_slot;          /* 15 */
+  /* costs (community.py:63) and reward (agent.py:230) */
+  float minutes_per_hour; /* 60 */
+  float kilo;             /* f32(1e-3) */
+  float penalty_weight;   /* 10 */
+  uint64_t seed;          /* Philox key */
+  int64_t scenario_offset; /* global index of this context's scenario 0 (multi-GPU sharding):
+                              Philox counters use global agent ids so results do not depend
+                              on how scenarios are split over ranks */
+} p2pmg_config;
+
+typedef struct p2pmg_episode_args {
+  int32_t mode;     /* P2PMG_MODE_TRAIN | P2PMG_MODE_GREEDY */
+  int32_t rng;      /* P2PMG_RNG_REPLAY | P2PMG_RNG_PHILOX (TRAIN only) */
+  int32_t episode;  /* episode index (Philox counter) */
+  int32_t record;   /* P2PMG_REC_* mask */
+  double epsilon;   /* exploration rate shared by every agent (QActor._epsilon) */
+} p2pmg_episode_args;
+
+/* version / defaults */
+int p2pmg_abi_version(void);
+int p2pmg_config_default(p2pmg_config* cfg); /* the reference constants, S = 1, N = 2, R = 1, T = 96 */
+
+/* lifetime */
+int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out);
+int p2pmg_destroy(p2pmg_ctx* ctx);
+const char* p2pmg_last_error(const p2pmg_ctx* ctx);
+int p2pmg_sync(p2pmg_ctx* ctx);
+int p2pmg_device_info(p2pmg_ctx* ctx, char* name, size_t name_len, size_t* total_mem);
+
+/* inputs (host arrays, copied to HBM) */
+int p2pmg_set_env(p2pmg_ctx* ctx, int n_env, const float* time, const float* t_out,
+                  const float* price_buy, const float* price_inj, const float* price_p2p);
+                  /* each [n_env][T], n_env in {1, S} */
+int p2pmg_set_profiles(p2pmg_ctx* ctx, const float* load_w, const float* pv_w); /* [A][T], A = S*N */
+int p2pmg_set_agent_params(p2pmg_ctx* ctx, const float* max_in);              /* [A] */
+int p2pmg_set_temperatures(p2pmg_ctx* ctx, const float* t_in, const float* t_m); /* [A] */
+int p2pmg_get_temperatures(p2pmg_ctx* ctx, float* t_in, float* t_m);
+int p2pmg_reset_temperatures_philox(p2pmg_ctx* ctx, int episode, double sigma); /* T0 ~ N(setpoint, sigma) */
+int p2pmg_set_replay_codes(p2pmg_ctx* ctx, const uint8_t* codes);            /* [T][R+1][A] */
+
+/* Q-tables in the reference layout (n_time, n_temp, n_bal, n_p2p, n_actions) per agent */
+int p2pmg_zero_q(p2pmg_ctx* ctx);
+int p2pmg_set_q(p2pmg_ctx* ctx, int first_agent, int count, const void* host, int host_dtype);
+int p2pmg_get_q(p2pmg_ctx* ctx, int first_agent, int count, void* host, int host_dtype);
+
+/* the hot path */
+int p2pmg_run_episode(p2pmg_ctx* ctx, const p2pmg_episode_args* args);
+int p2pmg_get_record(p2pmg_ctx* ctx, int which, void* host);   /* one P2PMG_REC_* bit */
+int p2pmg_get_episode_reward(p2pmg_ctx* ctx, float* host);     /* [S]: sum_t mean_i r (community.py:179) */
+int p2pmg_last_kernel_ms(p2pmg_ctx* ctx, float* ms);           /* HIP-event time of the last episode kernel */
+
+/* batched primitives (device) for unit parity against the reference functions */
+int p2pmg_rc_step(p2pmg_ctx* ctx, int n, const float* t_out, const float* t_in, const float* t_m,
+                  const float* hp, float* t_in_new, float* t_m_new);
+int p2pmg_state_indices(p2pmg_ctx* ctx, int n, const float* obs /* [n][4] */, int32_t* idx /* [n][4] */);
+
+/* host-only: decode a block of legacy-MT19937 32-bit words into replay codes, consuming words
+ * exactly as rand() (2 words) and choice(3) (masked rejection, 1 word per try) do.
+ * eps for decision k is eps[k % n_eps].  Returns P2PMG_E_INVALID if the words run out. */
+int p2pmg_replay_decode(const uint32_t* words, size_t n_words, size_t n_decisions,
+                        const double* eps, size_t n_eps, uint8_t* codes, size_t* consumed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* P2PMG_H */

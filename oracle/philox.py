@@ -1,0 +1,83 @@
+"""Philox4x32-10 counter-based RNG in NumPy — TEST INFRASTRUCTURE ONLY.
+
+This module is part of ``oracle/``: it is the checker for the device-side Philox
+exploration stream, never imported by the product (``p2pmicrogrid_amd``).
+
+The reference draws exploration from the global legacy ``np.random`` MT19937 stream
+(``microgrid/rl.py:101-111``); that order is reproduced by replay mode
+(``oracle/restatement.py``).  Philox mode is the build-defined, counter-keyed stream of
+SURVEY.md §3.5 (ii): one Philox block per (seed, episode, agent, t, round, tag), so the
+result is independent of how scenarios are sharded over GPUs.
+
+Block layout (must match ``p2pmicrogrid_amd/csrc/p2pmg.hip::philox_decision``):
+    key  = (seed_lo, seed_hi)
+    ctr  = (t * (R + 1) + r, episode, agent_global, TAG)
+    u    = ((x0 >> 5) * 2**26 + (x1 >> 6)) / 2**53          (NumPy's rand() formula)
+    act  = (x2 * 3) >> 32                                     (multiply-high, 3 actions)
+    explore <=> u < epsilon   (f64 compare, as rl.py:101)
+T0 draws at an episode start (tag TAG_T0, ctr = (0, episode, agent, TAG_T0)):
+    Box-Muller in f64 on u1 = (x0 + 0.5) / 2**32, u2 = (x1 + 0.5) / 2**32;
+    T_in = f32(setpoint + 0.3 * z0), T_m = f32(setpoint + 0.3 * z1)   (heating.py:149-152)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M0 = np.uint64(0xD2511F53)
+M1 = np.uint64(0xCD9E8D57)
+W0 = np.uint64(0x9E3779B9)
+W1 = np.uint64(0xBB67AE85)
+MASK32 = np.uint64(0xFFFFFFFF)
+
+TAG_DECISION = 0x5EED0001
+TAG_T0 = 0x5EED0002
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Vectorised Philox4x32-10 (Random123 definition). All args uint32-valued arrays."""
+    c0 = np.asarray(c0, dtype=np.uint64) & MASK32
+    c1 = np.asarray(c1, dtype=np.uint64) & MASK32
+    c2 = np.asarray(c2, dtype=np.uint64) & MASK32
+    c3 = np.asarray(c3, dtype=np.uint64) & MASK32
+    k0 = np.asarray(k0, dtype=np.uint64) & MASK32
+    k1 = np.asarray(k1, dtype=np.uint64) & MASK32
+    c0, c1, c2, c3, k0, k1 = np.broadcast_arrays(c0, c1, c2, c3, k0, k1)
+    c0, c1, c2, c3, k0, k1 = (x.copy() for x in (c0, c1, c2, c3, k0, k1))
+    for rnd in range(10):
+        if rnd > 0:
+            k0 = (k0 + W0) & MASK32
+            k1 = (k1 + W1) & MASK32
+        p0 = M0 * c0
+        p1 = M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & MASK32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & MASK32
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & MASK32, lo1, (hi0 ^ c3 ^ k1) & MASK32, lo0
+    return c0, c1, c2, c3
+
+
+def decision_draws(seed: int, episode: int, agents, t: int, r: int, rounds: int):
+    """(u f64, action int) for each agent id in ``agents`` at (episode, t, r)."""
+    agents = np.asarray(agents, dtype=np.uint64)
+    k0 = seed & 0xFFFFFFFF
+    k1 = (seed >> 32) & 0xFFFFFFFF
+    x0, x1, x2, _ = philox4x32_10(t * (rounds + 1) + r, episode, agents, TAG_DECISION, k0, k1)
+    a = (x0 >> np.uint64(5)).astype(np.float64)
+    b = (x1 >> np.uint64(6)).astype(np.float64)
+    u = (a * 67108864.0 + b) / 9007199254740992.0
+    act = ((x2 * np.uint64(3)) >> np.uint64(32)).astype(np.int64)
+    return u, act
+
+
+def t0_draws(seed: int, episode: int, agents, setpoint: float = 21.0, sigma: float = 0.3):
+    """(T_in f32, T_m f32) initial temperatures for an episode start in Philox mode."""
+    agents = np.asarray(agents, dtype=np.uint64)
+    k0 = seed & 0xFFFFFFFF
+    k1 = (seed >> 32) & 0xFFFFFFFF
+    x0, x1, _, _ = philox4x32_10(0, episode, agents, TAG_T0, k0, k1)
+    u1 = (x0.astype(np.float64) + 0.5) / 4294967296.0
+    u2 = (x1.astype(np.float64) + 0.5) / 4294967296.0
+    rad = np.sqrt(-2.0 * np.log(u1))
+    ang = 6.283185307179586 * u2
+    z0 = rad * np.cos(ang)
+    z1 = rad * np.sin(ang)
+    return (setpoint + sigma * z0).astype(np.float32), (setpoint + sigma * z1).astype(np.float32)

@@ -1,0 +1,63 @@
+// Internal declarations shared by p2pmg_kernels.hip (device code + launchers) and
+// p2pmg_runtime.cpp (context, C ABI).  Not part of the public ABI (include/p2pmg.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace p2pmg {
+
+constexpr int kEnvStride = 8;  // floats per env row: time, t_out, buy, inj, p2p, pad x3
+constexpr int kQPad = 4;       // Q row padded to 4 actions: 32-B (f64) / 16-B (f32) aligned rows
+constexpr int kWave = 64;      // one wave per workgroup
+constexpr int kMaxAgents = 16; // compiled-in agents per scenario
+
+// Everything the episode kernel needs, passed by value in the kernarg segment.
+struct EpisodeParams {
+  int S, N, R, T, A;
+  int mode, rng, episode, record;
+  int n_env;                 // 1 (shared environment) or S (one per scenario)
+  const float* env;          // [T][n_env][kEnvStride] time-major
+  const float2* prof;        // [T][A] {load_w, pv_w}
+  const float* max_in;       // [A]
+  float* t_in;               // [A] in/out
+  float* t_m;                // [A] in/out
+  void* q;                   // [A][n_states][kQPad] f64 | f32
+  const uint8_t* codes;      // [T][R+1][A] replay codes
+  double eps;
+  uint32_t seed_lo, seed_hi;
+  uint32_t agent_offset;     // global id of local agent 0 (Philox counter)
+  float* rec_reward;         // [T][A]
+  float* rec_cost;
+  float* rec_grid;
+  float* rec_p2p;
+  float* rec_tin;
+  uint8_t* rec_action;       // [T][R+1][A]
+  int32_t* rec_index;        // [T][R+1][A]
+  float* ep_reward;          // [S]
+  int nt, nT, nb, np;
+  double alpha, gamma;
+  float hp_levels[4];
+  float setpoint, margin, lower, upper;
+  float inv_ci, inv_cm, inv_ri, inv_re, inv_rvent, c_in, c_m, solar, cop, spm, slot;
+  float mph, kilo, penw;
+};
+
+struct RcParams {
+  float inv_ci, inv_cm, inv_ri, inv_re, inv_rvent, c_in, c_m, solar, cop, spm, slot;
+};
+
+hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream);
+hipError_t launch_rc_step(int n, const float* t_out, const float* t_in, const float* t_m, const float* hp,
+                          float* t_in_new, float* t_m_new, RcParams rc, hipStream_t stream);
+hipError_t launch_state_indices(int n, const float* obs, int32_t* idx, int nt, int nT, int nb, int np,
+                                hipStream_t stream);
+hipError_t launch_t0_philox(int A, float* t_in, float* t_m, uint32_t seed_lo, uint32_t seed_hi, int episode,
+                            uint32_t agent_offset, float setpoint, double sigma, hipStream_t stream);
+hipError_t launch_q_pack(int count, size_t n_states, int n_actions, const void* src_ref, void* dst_pad,
+                         int q_dtype, int src_dtype, hipStream_t stream);
+hipError_t launch_q_unpack(int count, size_t n_states, int n_actions, const void* src_pad, void* dst_ref,
+                           int q_dtype, int dst_dtype, hipStream_t stream);
+hipError_t launch_prof_pack(int A, int T, const float* load_w, const float* pv_w, float2* prof,
+                            hipStream_t stream);
+
+}  // namespace p2pmg

@@ -1,0 +1,541 @@
+// p2pmg_runtime.cpp — context, device buffers and the extern "C" ABI of libp2pmg.so
+// (declared in include/p2pmg.h).  No C++ exception crosses the ABI: every entry point
+// returns a status and records a message in the context.
+#include "p2pmg.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "p2pmg_internal.h"
+
+using p2pmg::EpisodeParams;
+using p2pmg::kEnvStride;
+using p2pmg::kQPad;
+
+struct p2pmg_ctx {
+  p2pmg_config cfg{};
+  int device = 0;
+  int S = 0, N = 0, R = 0, T = 0, A = 0;
+  size_t n_states = 0;
+  size_t q_elem = 8;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  // device buffers
+  float* env = nullptr;
+  int n_env = 0;
+  float2* prof = nullptr;
+  float* max_in = nullptr;
+  float* t_in = nullptr;
+  float* t_m = nullptr;
+  void* q = nullptr;
+  uint8_t* codes = nullptr;
+  float* ep_reward = nullptr;
+  float* rec_f32[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // reward, cost, grid, p2p, tin
+  uint8_t* rec_action = nullptr;
+  int32_t* rec_index = nullptr;
+  bool have_env = false, have_prof = false, have_params = false, have_codes = false;
+  std::string err;
+};
+
+namespace {
+
+int fail(p2pmg_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                       \
+  do {                                                                                           \
+    hipError_t _e = (expr);                                                                      \
+    if (_e != hipSuccess)                                                                        \
+      return fail((ctx), _e == hipErrorOutOfMemory ? P2PMG_E_NOMEM : P2PMG_E_HIP,                \
+                  std::string(#expr) + ": " + hipGetErrorString(_e));                            \
+  } while (0)
+
+template <typename T>
+hipError_t dmalloc(T** p, size_t n) {
+  return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T) > 0 ? n * sizeof(T) : 16);
+}
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(reinterpret_cast<void*>(p));
+  p = nullptr;
+}
+
+int rec_slot(int which) {
+  switch (which) {
+    case P2PMG_REC_REWARD: return 0;
+    case P2PMG_REC_COST: return 1;
+    case P2PMG_REC_GRID: return 2;
+    case P2PMG_REC_P2P: return 3;
+    case P2PMG_REC_TEMP: return 4;
+    default: return -1;
+  }
+}
+
+// Ensure every record buffer requested in mask exists (lazily allocated, kept for reuse).
+int ensure_records(p2pmg_ctx* c, int mask) {
+  const size_t ta = (size_t)c->T * c->A;
+  for (int b = 0; b < 5; ++b)
+    if ((mask & (1 << b)) && !c->rec_f32[b]) HIP_TRY(c, dmalloc(&c->rec_f32[b], ta));
+  const size_t tra = (size_t)c->T * (c->R + 1) * c->A;
+  if ((mask & P2PMG_REC_ACTION) && !c->rec_action) HIP_TRY(c, dmalloc(&c->rec_action, tra));
+  if ((mask & P2PMG_REC_INDEX) && !c->rec_index) HIP_TRY(c, dmalloc(&c->rec_index, tra));
+  return P2PMG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int p2pmg_abi_version(void) { return P2PMG_ABI_VERSION; }
+
+int p2pmg_config_default(p2pmg_config* cfg) {
+  if (!cfg) return P2PMG_E_INVALID;
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->n_scenarios = 1;
+  cfg->n_agents = 2;   // setup.py:33
+  cfg->rounds = 1;     // setup.py:34
+  cfg->horizon = 96;   // one day of 15-minute slots
+  cfg->q_dtype = P2PMG_Q_F64;
+  cfg->n_time_states = cfg->n_temp_states = cfg->n_balance_states = cfg->n_p2p_states = 20;
+  cfg->n_actions = 3;
+  cfg->alpha = 1e-5;
+  cfg->gamma = 0.9;
+  const double levels[3] = {0.0, 0.5, 1.0};
+  for (int k = 0; k < 3; ++k) cfg->hp_levels[k] = (float)(levels[k] * 3e3);
+  cfg->setpoint = 21.0f;
+  cfg->temp_margin = 1.0f;
+  cfg->lower_bound = 20.0f;
+  cfg->upper_bound = 22.0f;
+  const double Ci = 2.44e6 * 2, Cm = 9.4e7, Ri = 8.64e-4, Re = 1.05e-2, Rvent = 7.98e-3, gA = 11.468, f_rad = 0.3;
+  cfg->inv_ci = (float)(1 / Ci);
+  cfg->inv_cm = (float)(1 / Cm);
+  cfg->inv_ri = (float)(1 / Ri);
+  cfg->inv_re = (float)(1 / Re);
+  cfg->inv_rvent = (float)(1 / Rvent);
+  cfg->one_minus_frad = (float)(1 - f_rad);
+  cfg->frad = (float)f_rad;
+  cfg->solar_gain = (float)(gA * 0.0);
+  cfg->hp_cop = 3.0f;
+  cfg->seconds_per_minute = 60.0f;
+  cfg->time_slot = 15.0f;
+  cfg->minutes_per_hour = 60.0f;
+  cfg->kilo = (float)1e-3;
+  cfg->penalty_weight = 10.0f;
+  cfg->seed = 42;
+  cfg->scenario_offset = 0;
+  return P2PMG_OK;
+}
+
+int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
+  if (!cfg || !out) return P2PMG_E_INVALID;
+  *out = nullptr;
+  if (cfg->n_scenarios <= 0 || cfg->n_agents <= 0 || cfg->rounds < 0 || cfg->horizon <= 0) return P2PMG_E_INVALID;
+  if (cfg->n_actions != 3) return P2PMG_E_UNSUPPORTED;
+  const int N = cfg->n_agents;
+  if (!((N >= 1 && N <= 8) || N == 16)) return P2PMG_E_UNSUPPORTED;
+  if (cfg->q_dtype != P2PMG_Q_F64 && cfg->q_dtype != P2PMG_Q_F32) return P2PMG_E_INVALID;
+  p2pmg_ctx* c = new (std::nothrow) p2pmg_ctx();
+  if (!c) return P2PMG_E_NOMEM;
+  c->cfg = *cfg;
+  c->device = device;
+  c->S = cfg->n_scenarios;
+  c->N = N;
+  c->R = cfg->rounds;
+  c->T = cfg->horizon;
+  c->A = c->S * c->N;
+  c->n_states = (size_t)cfg->n_time_states * cfg->n_temp_states * cfg->n_balance_states * cfg->n_p2p_states;
+  c->q_elem = cfg->q_dtype == P2PMG_Q_F64 ? 8 : 4;
+  auto bail = [&](int code) {
+    p2pmg_destroy(c);
+    return code;
+  };
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return bail(P2PMG_E_HIP);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(P2PMG_E_HIP);
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) return bail(P2PMG_E_HIP);
+  const size_t A = (size_t)c->A;
+  if (dmalloc(&c->prof, (size_t)c->T * A) != hipSuccess || dmalloc(&c->max_in, A) != hipSuccess ||
+      dmalloc(&c->t_in, A) != hipSuccess || dmalloc(&c->t_m, A) != hipSuccess ||
+      dmalloc(&c->ep_reward, (size_t)c->S) != hipSuccess)
+    return bail(P2PMG_E_NOMEM);
+  const size_t qbytes = A * c->n_states * kQPad * c->q_elem;
+  if (hipMalloc(&c->q, qbytes) != hipSuccess) return bail(P2PMG_E_NOMEM);
+  if (hipMemsetAsync(c->q, 0, qbytes, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
+  std::vector<float> t0(A, cfg->setpoint);
+  if (hipMemcpyAsync(c->t_in, t0.data(), A * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(c->t_m, t0.data(), A * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return bail(P2PMG_E_HIP);
+  *out = c;
+  return P2PMG_OK;
+}
+
+int p2pmg_destroy(p2pmg_ctx* c) {
+  if (!c) return P2PMG_OK;
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  dfree(c->env);
+  dfree(c->prof);
+  dfree(c->max_in);
+  dfree(c->t_in);
+  dfree(c->t_m);
+  if (c->q) (void)hipFree(c->q);
+  dfree(c->codes);
+  dfree(c->ep_reward);
+  for (auto& b : c->rec_f32) dfree(b);
+  dfree(c->rec_action);
+  dfree(c->rec_index);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return P2PMG_OK;
+}
+
+const char* p2pmg_last_error(const p2pmg_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int p2pmg_sync(p2pmg_ctx* c) {
+  if (!c) return P2PMG_E_INVALID;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_device_info(p2pmg_ctx* c, char* name, size_t name_len, size_t* total_mem) {
+  if (!c) return P2PMG_E_INVALID;
+  hipDeviceProp_t prop;
+  HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
+  if (name && name_len) {
+    std::snprintf(name, name_len, "%s (%s)", prop.name, prop.gcnArchName);
+  }
+  if (total_mem) *total_mem = prop.totalGlobalMem;
+  return P2PMG_OK;
+}
+
+int p2pmg_set_env(p2pmg_ctx* c, int n_env, const float* time, const float* t_out, const float* buy, const float* inj,
+                  const float* p2p) {
+  if (!c || !time || !t_out || !buy || !inj || !p2p) return P2PMG_E_INVALID;
+  if (n_env != 1 && n_env != c->S) return fail(c, P2PMG_E_INVALID, "n_env must be 1 or S");
+  const size_t T = c->T;
+  std::vector<float> h((size_t)n_env * T * kEnvStride, 0.0f);
+  for (int s = 0; s < n_env; ++s)
+    for (size_t t = 0; t < T; ++t) {
+      float* r = &h[((size_t)t * n_env + s) * kEnvStride];  // time-major [T][n_env][8]
+      const size_t k = (size_t)s * T + t;
+      r[0] = time[k];
+      r[1] = t_out[k];
+      r[2] = buy[k];
+      r[3] = inj[k];
+      r[4] = p2p[k];
+    }
+  if (c->n_env != n_env) {
+    dfree(c->env);
+    HIP_TRY(c, dmalloc(&c->env, h.size()));
+    c->n_env = n_env;
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->env, h.data(), h.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->have_env = true;
+  return P2PMG_OK;
+}
+
+int p2pmg_set_profiles(p2pmg_ctx* c, const float* load_w, const float* pv_w) {
+  if (!c || !load_w || !pv_w) return P2PMG_E_INVALID;
+  const size_t n = (size_t)c->A * c->T;
+  float *dl = nullptr, *dp = nullptr;
+  HIP_TRY(c, dmalloc(&dl, n));
+  hipError_t e = dmalloc(&dp, n);
+  if (e != hipSuccess) {
+    dfree(dl);
+    return fail(c, P2PMG_E_NOMEM, "profile staging");
+  }
+  e = hipMemcpyAsync(dl, load_w, n * 4, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dp, pv_w, n * 4, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = p2pmg::launch_prof_pack(c->A, c->T, dl, dp, c->prof, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(dl);
+  dfree(dp);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("set_profiles: ") + hipGetErrorString(e));
+  c->have_prof = true;
+  return P2PMG_OK;
+}
+
+int p2pmg_set_agent_params(p2pmg_ctx* c, const float* max_in) {
+  if (!c || !max_in) return P2PMG_E_INVALID;
+  HIP_TRY(c, hipMemcpyAsync(c->max_in, max_in, (size_t)c->A * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->have_params = true;
+  return P2PMG_OK;
+}
+
+int p2pmg_set_temperatures(p2pmg_ctx* c, const float* t_in, const float* t_m) {
+  if (!c || !t_in || !t_m) return P2PMG_E_INVALID;
+  HIP_TRY(c, hipMemcpyAsync(c->t_in, t_in, (size_t)c->A * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->t_m, t_m, (size_t)c->A * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_get_temperatures(p2pmg_ctx* c, float* t_in, float* t_m) {
+  if (!c || !t_in || !t_m) return P2PMG_E_INVALID;
+  HIP_TRY(c, hipMemcpyAsync(t_in, c->t_in, (size_t)c->A * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(t_m, c->t_m, (size_t)c->A * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_reset_temperatures_philox(p2pmg_ctx* c, int episode, double sigma) {
+  if (!c) return P2PMG_E_INVALID;
+  const uint32_t off = (uint32_t)(c->cfg.scenario_offset * c->N);
+  HIP_TRY(c, p2pmg::launch_t0_philox(c->A, c->t_in, c->t_m, (uint32_t)(c->cfg.seed & 0xFFFFFFFFu),
+                                     (uint32_t)(c->cfg.seed >> 32), episode, off, c->cfg.setpoint, sigma, c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_set_replay_codes(p2pmg_ctx* c, const uint8_t* codes) {
+  if (!c || !codes) return P2PMG_E_INVALID;
+  const size_t n = (size_t)c->T * (c->R + 1) * c->A;
+  if (!c->codes) HIP_TRY(c, dmalloc(&c->codes, n));
+  HIP_TRY(c, hipMemcpyAsync(c->codes, codes, n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->have_codes = true;
+  return P2PMG_OK;
+}
+
+int p2pmg_zero_q(p2pmg_ctx* c) {
+  if (!c) return P2PMG_E_INVALID;
+  HIP_TRY(c, hipMemsetAsync(c->q, 0, (size_t)c->A * c->n_states * kQPad * c->q_elem, c->stream));
+  return P2PMG_OK;
+}
+
+static int q_range_ok(p2pmg_ctx* c, int first, int count, const void* host, int dtype) {
+  if (!c || !host || first < 0 || count < 0 || first + count > c->A) return 0;
+  return dtype == P2PMG_Q_F64 || dtype == P2PMG_Q_F32;
+}
+
+int p2pmg_set_q(p2pmg_ctx* c, int first, int count, const void* host, int host_dtype) {
+  if (!q_range_ok(c, first, count, host, host_dtype)) return fail(c, P2PMG_E_INVALID, "set_q: bad range/dtype");
+  const int na = c->cfg.n_actions;
+  const size_t hbytes = (size_t)count * c->n_states * na * (host_dtype == P2PMG_Q_F64 ? 8 : 4);
+  void* staging = nullptr;
+  HIP_TRY(c, hipMalloc(&staging, hbytes ? hbytes : 16));
+  char* dst = static_cast<char*>(c->q) + (size_t)first * c->n_states * kQPad * c->q_elem;
+  hipError_t e = hipMemcpyAsync(staging, host, hbytes, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess)
+    e = p2pmg::launch_q_pack(count, c->n_states, na, staging, dst, c->cfg.q_dtype, host_dtype, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(staging);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("set_q: ") + hipGetErrorString(e));
+  return P2PMG_OK;
+}
+
+int p2pmg_get_q(p2pmg_ctx* c, int first, int count, void* host, int host_dtype) {
+  if (!q_range_ok(c, first, count, host, host_dtype)) return fail(c, P2PMG_E_INVALID, "get_q: bad range/dtype");
+  const int na = c->cfg.n_actions;
+  const size_t hbytes = (size_t)count * c->n_states * na * (host_dtype == P2PMG_Q_F64 ? 8 : 4);
+  void* staging = nullptr;
+  HIP_TRY(c, hipMalloc(&staging, hbytes ? hbytes : 16));
+  const char* src = static_cast<const char*>(c->q) + (size_t)first * c->n_states * kQPad * c->q_elem;
+  hipError_t e = p2pmg::launch_q_unpack(count, c->n_states, na, src, staging, c->cfg.q_dtype, host_dtype, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(host, staging, hbytes, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(staging);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("get_q: ") + hipGetErrorString(e));
+  return P2PMG_OK;
+}
+
+int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
+  if (!c || !args) return P2PMG_E_INVALID;
+  if (!c->have_env || !c->have_prof || !c->have_params)
+    return fail(c, P2PMG_E_STATE, "run_episode: env, profiles and agent params must be set first");
+  const bool train = args->mode == P2PMG_MODE_TRAIN;
+  if (args->mode != P2PMG_MODE_TRAIN && args->mode != P2PMG_MODE_GREEDY) return fail(c, P2PMG_E_INVALID, "mode");
+  if (train && args->rng != P2PMG_RNG_REPLAY && args->rng != P2PMG_RNG_PHILOX) return fail(c, P2PMG_E_INVALID, "rng");
+  if (train && args->rng == P2PMG_RNG_REPLAY && !c->have_codes)
+    return fail(c, P2PMG_E_STATE, "run_episode: replay mode needs p2pmg_set_replay_codes");
+  int rc = ensure_records(c, args->record);
+  if (rc != P2PMG_OK) return rc;
+  const p2pmg_config& g = c->cfg;
+  EpisodeParams p{};
+  p.S = c->S;
+  p.N = c->N;
+  p.R = c->R;
+  p.T = c->T;
+  p.A = c->A;
+  p.mode = args->mode;
+  p.rng = args->rng;
+  p.episode = args->episode;
+  p.record = args->record;
+  p.n_env = c->n_env;
+  p.env = c->env;
+  p.prof = c->prof;
+  p.max_in = c->max_in;
+  p.t_in = c->t_in;
+  p.t_m = c->t_m;
+  p.q = c->q;
+  p.codes = c->codes;
+  p.eps = args->epsilon;
+  p.seed_lo = (uint32_t)(g.seed & 0xFFFFFFFFu);
+  p.seed_hi = (uint32_t)(g.seed >> 32);
+  p.agent_offset = (uint32_t)(g.scenario_offset * c->N);
+  p.rec_reward = c->rec_f32[0];
+  p.rec_cost = c->rec_f32[1];
+  p.rec_grid = c->rec_f32[2];
+  p.rec_p2p = c->rec_f32[3];
+  p.rec_tin = c->rec_f32[4];
+  p.rec_action = c->rec_action;
+  p.rec_index = c->rec_index;
+  p.ep_reward = c->ep_reward;
+  p.nt = g.n_time_states;
+  p.nT = g.n_temp_states;
+  p.nb = g.n_balance_states;
+  p.np = g.n_p2p_states;
+  p.alpha = g.alpha;
+  p.gamma = g.gamma;
+  for (int k = 0; k < 4; ++k) p.hp_levels[k] = g.hp_levels[k];
+  p.setpoint = g.setpoint;
+  p.margin = g.temp_margin;
+  p.lower = g.lower_bound;
+  p.upper = g.upper_bound;
+  p.inv_ci = g.inv_ci;
+  p.inv_cm = g.inv_cm;
+  p.inv_ri = g.inv_ri;
+  p.inv_re = g.inv_re;
+  p.inv_rvent = g.inv_rvent;
+  p.c_in = g.one_minus_frad;
+  p.c_m = g.frad;
+  p.solar = g.solar_gain;
+  p.cop = g.hp_cop;
+  p.spm = g.seconds_per_minute;
+  p.slot = g.time_slot;
+  p.mph = g.minutes_per_hour;
+  p.kilo = g.kilo;
+  p.penw = g.penalty_weight;
+  HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
+  hipError_t e = p2pmg::launch_episode(p, g.q_dtype, c->stream);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));
+  HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  return P2PMG_OK;
+}
+
+int p2pmg_last_kernel_ms(p2pmg_ctx* c, float* ms) {
+  if (!c || !ms) return P2PMG_E_INVALID;
+  if (!c->timed) return fail(c, P2PMG_E_STATE, "no episode launched yet");
+  HIP_TRY(c, hipEventSynchronize(c->ev1));
+  HIP_TRY(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return P2PMG_OK;
+}
+
+int p2pmg_get_record(p2pmg_ctx* c, int which, void* host) {
+  if (!c || !host) return P2PMG_E_INVALID;
+  const size_t ta = (size_t)c->T * c->A;
+  const size_t tra = (size_t)c->T * (c->R + 1) * c->A;
+  const void* src = nullptr;
+  size_t bytes = 0;
+  const int slot = rec_slot(which);
+  if (slot >= 0) {
+    src = c->rec_f32[slot];
+    bytes = ta * 4;
+  } else if (which == P2PMG_REC_ACTION) {
+    src = c->rec_action;
+    bytes = tra;
+  } else if (which == P2PMG_REC_INDEX) {
+    src = c->rec_index;
+    bytes = tra * 4;
+  } else {
+    return fail(c, P2PMG_E_INVALID, "get_record: unknown record");
+  }
+  if (!src) return fail(c, P2PMG_E_STATE, "get_record: record was never requested");
+  HIP_TRY(c, hipMemcpyAsync(host, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_get_episode_reward(p2pmg_ctx* c, float* host) {
+  if (!c || !host) return P2PMG_E_INVALID;
+  HIP_TRY(c, hipMemcpyAsync(host, c->ep_reward, (size_t)c->S * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_rc_step(p2pmg_ctx* c, int n, const float* t_out, const float* t_in, const float* t_m, const float* hp,
+                  float* t_in_new, float* t_m_new) {
+  if (!c || n < 0 || !t_out || !t_in || !t_m || !hp || !t_in_new || !t_m_new) return P2PMG_E_INVALID;
+  if (n == 0) return P2PMG_OK;
+  float* d = nullptr;
+  HIP_TRY(c, dmalloc(&d, (size_t)6 * n));
+  const size_t b = (size_t)n * 4;
+  hipError_t e = hipMemcpyAsync(d, t_out, b, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + n, t_in, b, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + 2 * (size_t)n, t_m, b, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + 3 * (size_t)n, hp, b, hipMemcpyHostToDevice, c->stream);
+  const p2pmg_config& g = c->cfg;
+  p2pmg::RcParams rc{g.inv_ci, g.inv_cm, g.inv_ri, g.inv_re, g.inv_rvent, g.one_minus_frad,
+                     g.frad, g.solar_gain, g.hp_cop, g.seconds_per_minute, g.time_slot};
+  if (e == hipSuccess)
+    e = p2pmg::launch_rc_step(n, d, d + n, d + 2 * (size_t)n, d + 3 * (size_t)n, d + 4 * (size_t)n,
+                              d + 5 * (size_t)n, rc, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(t_in_new, d + 4 * (size_t)n, b, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(t_m_new, d + 5 * (size_t)n, b, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(d);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("rc_step: ") + hipGetErrorString(e));
+  return P2PMG_OK;
+}
+
+int p2pmg_state_indices(p2pmg_ctx* c, int n, const float* obs, int32_t* idx) {
+  if (!c || n < 0 || !obs || !idx) return P2PMG_E_INVALID;
+  if (n == 0) return P2PMG_OK;
+  float* d = nullptr;
+  int32_t* di = nullptr;
+  HIP_TRY(c, dmalloc(&d, (size_t)4 * n));
+  hipError_t e = dmalloc(&di, (size_t)4 * n);
+  if (e == hipSuccess) e = hipMemcpyAsync(d, obs, (size_t)16 * n, hipMemcpyHostToDevice, c->stream);
+  const p2pmg_config& g = c->cfg;
+  if (e == hipSuccess)
+    e = p2pmg::launch_state_indices(n, d, di, g.n_time_states, g.n_temp_states, g.n_balance_states, g.n_p2p_states,
+                                    c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(idx, di, (size_t)16 * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(d);
+  dfree(di);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("state_indices: ") + hipGetErrorString(e));
+  return P2PMG_OK;
+}
+
+int p2pmg_replay_decode(const uint32_t* words, size_t n_words, size_t n_decisions, const double* eps, size_t n_eps,
+                        uint8_t* codes, size_t* consumed) {
+  if (!words || !eps || n_eps == 0 || !codes) return P2PMG_E_INVALID;
+  size_t pos = 0;
+  for (size_t k = 0; k < n_decisions; ++k) {
+    // RandomState.rand(): (a * 2^26 + b) / 2^53 with a = w0 >> 5, b = w1 >> 6 (mt19937 next_double)
+    if (pos + 2 > n_words) return P2PMG_E_INVALID;
+    const uint32_t a = words[pos] >> 5, b = words[pos + 1] >> 6;
+    pos += 2;
+    const double u = ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+    if (u < eps[k % n_eps]) {
+      // RandomState.choice(3) -> randint(0, 3): masked rejection, mask 3, one word per try
+      uint32_t v;
+      do {
+        if (pos >= n_words) return P2PMG_E_INVALID;
+        v = words[pos++] & 3u;
+      } while (v > 2u);
+      codes[k] = (uint8_t)v;
+    } else {
+      codes[k] = P2PMG_GREEDY;
+    }
+  }
+  if (consumed) *consumed = pos;
+  return P2PMG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+"""Profiles with the reference's schema (mirrors microgrid/dataset.py).
+
+The reference reads a private SQLite database filled from a credentialed REST API
+(dataset.py:61-80, database.py:128-147); neither is available, so this module generates
+synthetic data with the SAME schema and splits:
+
+  time        slot / 96 in [0, 1)                       (dataset.py:43-44)
+  temperature outdoor temperature, degC (not normalised)
+  pv          PV shape normalised by its max             (dataset.py:50)
+  l0..l4      five household loads normalised by max    (dataset.py:30, 46-48)
+
+``dataframe_to_dataset`` returns a ``ProfileDataset`` holding the f32 array and its
+``np.roll(-1)`` partner (dataset.py:98-103), which is what the environment and agents stream.
+``scenario_batch`` builds the device inputs for S independent communities at once.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import numpy as np
+import pandas as pd
+
+from . import setup
+
+# Data splits (dataset.py:17-25)
+data_month = 10
+testing_days = [8, 9, 10, 19, 20]
+validation_days = [18]
+training_days = list(range(11, 18))
+
+env_cols = ['day', 'time', 'temperature']
+agent_cols = ['pv']
+load_cols = ['l0', 'l1', 'l2', 'l3', 'l4']
+cols = env_cols + agent_cols + load_cols
+
+SLOTS_PER_DAY = setup.HOURS_PER_DAY * setup.MINUTES_PER_HOUR // setup.TIME_SLOT  # 96
+
+
+def _day_profiles(rs: np.random.RandomState, days: np.ndarray, shape_prefix=()):
+    """Vectorised synthetic day profiles for the given day numbers -> dict of arrays [..., D*96]."""
+    D = len(days)
+    T = D * SLOTS_PER_DAY
+    slot = np.arange(T) % SLOTS_PER_DAY
+    hour = slot / 4.0
+    day = np.arange(T) // SLOTS_PER_DAY
+    sp = tuple(shape_prefix)
+    day_temp = 8.0 + 4.0 * np.sin(2 * np.pi * (np.asarray(days) - 5) / 30.0)
+    temp = (day_temp[day] + 5.0 * np.sin(2 * np.pi * (hour - 9.0) / 24.0)
+            + rs.normal(0.0, 1.0, sp + (T,)))
+    cloud = 0.55 + 0.45 * rs.rand(*(sp + (D,)))
+    pv = np.clip(np.sin(np.pi * (hour - 7.0) / 10.0), 0, None) * np.take(cloud, day, axis=-1)
+    loads = []
+    for k in range(5):
+        m = (0.25 + 0.35 * np.exp(-((hour - (7.5 + 0.3 * k)) ** 2) / 2.0)
+             + 0.6 * np.exp(-((hour - (19.0 + 0.25 * k)) ** 2) / 3.0) + 0.15 * rs.rand(*(sp + (T,))))
+        loads.append(m)
+    return dict(time=slot / float(SLOTS_PER_DAY), temperature=temp, pv=pv, loads=np.stack(loads, axis=-2))
+
+
+def get_data(days: List[int], seed: int = 2021) -> Tuple[pd.DataFrame, List[pd.DataFrame]]:
+    """Synthetic stand-in for dataset.get_data (dataset.py:61-80): same columns and
+    normalisation; one frame per load column renamed to 'load' (dataset.py:78)."""
+    rs = np.random.RandomState(seed + 1000 * min(days))
+    prof = _day_profiles(rs, np.asarray(days))
+    df = pd.DataFrame({
+        'day': np.repeat(days, SLOTS_PER_DAY),
+        'time': prof['time'],
+        'temperature': prof['temperature'],
+        'pv': prof['pv'] / prof['pv'].max(),
+    })
+    for k, c in enumerate(load_cols):
+        df[c] = prof['loads'][k] / prof['loads'][k].max()
+    df = df[cols]
+    agent_dfs = [df[[l] + agent_cols].rename(columns={l: 'load'}) for l in load_cols]
+    return df[env_cols], agent_dfs
+
+
+def get_train_data() -> Tuple[pd.DataFrame, List[pd.DataFrame]]:
+    env_df, agent_dfs = get_data(training_days)
+    env_df = env_df.drop(axis=1, labels='day')
+    return env_df, agent_dfs
+
+
+def get_validation_data() -> Tuple[pd.DataFrame, List[pd.DataFrame]]:
+    return get_data(validation_days)
+
+
+def get_test_data() -> Tuple[pd.DataFrame, List[pd.DataFrame]]:
+    return get_data(testing_days)
+
+
+@dataclass
+class ProfileDataset:
+    """(x_t, x_{t+1}) pairs of an f32 table, as tf.data.Dataset.from_tensor_slices((data,
+    np.roll(data, -1))) in dataset.py:98-103."""
+    data: np.ndarray
+    rolled: np.ndarray
+
+    def __len__(self):
+        return len(self.data)
+
+    def __iter__(self):
+        return iter(zip(self.data, self.rolled))
+
+    @property
+    def current(self) -> np.ndarray:
+        return self.data
+
+
+def dataframe_to_dataset(df, roll_len: int = -1, axis: int = 0) -> ProfileDataset:
+    data = np.array(df, dtype=np.float32)
+    return ProfileDataset(data, np.roll(data, roll_len, axis=axis))
+
+
+# ----------------------------------------------------------------------------- batched scenarios
+@dataclass
+class ScenarioInputs:
+    """Device inputs for S independent communities (SURVEY.md §8d synthetic inputs)."""
+    time: np.ndarray      # [T] f32
+    t_out: np.ndarray     # [S, T] f32 (per-scenario weather) or [1, T]
+    load_w: np.ndarray    # [S, N, T] f32
+    pv_w: np.ndarray      # [S, N, T] f32
+    max_in: np.ndarray    # [S, N] f32
+    t_in0: np.ndarray     # [S, N] f32
+    t_m0: np.ndarray      # [S, N] f32
+    load_ratings: np.ndarray
+    pv_ratings: np.ndarray
+
+
+_BLOCK = 256  # scenarios per generator block: a scenario's data depends only on (seed, s)
+
+
+def _scenario_block(seed: int, block: int, N: int, T: int, homogeneous: bool):
+    days = np.arange(T // SLOTS_PER_DAY + (T % SLOTS_PER_DAY > 0)) + training_days[0]
+    rs = np.random.RandomState((seed * 1_000_003 + block * 7_919 + 17) % (2 ** 32))
+    prof = _day_profiles(rs, days, shape_prefix=(_BLOCK,))
+    # normalise over the whole generated days (dataset.py:46-50), then cut to the horizon
+    pv = (prof['pv'] / prof['pv'].max(axis=-1, keepdims=True))[..., :T]
+    loads = (prof['loads'] / prof['loads'].max(axis=-1, keepdims=True))[..., :T]
+    t_out = prof['temperature'][..., :T].astype(np.float32)
+    if homogeneous:
+        lr = np.full((_BLOCK, N), 0.7)
+        pr = np.full((_BLOCK, N), 4.0)
+        t_in0 = np.full((_BLOCK, N), np.float32(21.0), np.float32)
+        t_m0 = t_in0.copy()
+    else:
+        lr = rs.normal(0.7, 0.2, (_BLOCK, N))
+        pr = rs.normal(4, 0.2, (_BLOCK, N))
+        t_m0 = rs.normal(21.0, 0.3, (_BLOCK, N)).astype(np.float32)
+        t_in0 = rs.normal(21.0, 0.3, (_BLOCK, N)).astype(np.float32)
+    cols_idx = np.arange(N) % 5
+    load_w = ((loads[:, cols_idx, :] * lr[..., None]) * 1e3).astype(np.float32)
+    pv_w = ((pv[:, None, :] * pr[..., None]) * 1e3).astype(np.float32)
+    max_in = (np.maximum(lr, pr) * 1.1 * 1e3).astype(np.float32)
+    return dict(t_out=t_out, load_w=load_w, pv_w=pv_w, max_in=max_in, t_in0=t_in0, t_m0=t_m0,
+                load_ratings=lr, pv_ratings=pr)
+
+
+def scenario_batch(S: int, N: int, T: int = SLOTS_PER_DAY, seed: int = setup.seed, homogeneous: bool = False,
+                   shared_weather: bool = False, first_scenario: int = 0) -> ScenarioInputs:
+    """Scenarios [first_scenario, first_scenario + S) of N agents, built as get_community does
+    (community.py:198-234): ratings ~ N(0.7, 0.2) kW / N(4, 0.2) kW, max_in = max(load_kW,
+    pv_kW) * 1.1e3, W profiles = f32((norm * rating) * 1e3), T0 ~ N(21, 0.3) (heterogeneous).
+    Agent i uses load column l_{i mod 5} (the reference has 5, dataset.py:30).
+    Scenario s's data depends only on (seed, s), so any shard of a multi-GPU run is generated
+    alone and matches the single-GPU batch."""
+    b0, b1 = first_scenario // _BLOCK, (first_scenario + S - 1) // _BLOCK
+    parts = [_scenario_block(seed, b, N, T, homogeneous) for b in range(b0, b1 + 1)]
+    cat = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    lo = first_scenario - b0 * _BLOCK
+    sl = {k: np.ascontiguousarray(v[lo:lo + S]) for k, v in cat.items()}
+    time = (np.arange(T) % SLOTS_PER_DAY / float(SLOTS_PER_DAY)).astype(np.float32)
+    t_out = sl['t_out'][:1] if shared_weather else sl['t_out']
+    return ScenarioInputs(time=time, t_out=t_out, load_w=sl['load_w'], pv_w=sl['pv_w'], max_in=sl['max_in'],
+                          t_in0=sl['t_in0'], t_m0=sl['t_m0'], load_ratings=sl['load_ratings'],
+                          pv_ratings=sl['pv_ratings'])

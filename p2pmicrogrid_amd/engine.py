@@ -1,0 +1,215 @@
+"""DeviceCommunityBatch — S independent communities x N agents resident in HBM.
+
+This is the batched entry point the reference lacks (SURVEY.md §8b "Add a batched entry
+point over S scenarios"): one ``run_episode`` call is one ``CommunityMicrogrid.train_episode``
+(community.py:149-182) or ``run`` (community.py:95-123) for every scenario at once, executed
+by ONE HIP kernel launch (p2pmg_kernels.hip::episode_kernel).  The reference-shaped object API
+(``community.CommunityMicrogrid`` & co.) is a thin layer over this class with S = 1.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from . import setup as cfgmod
+
+F32 = np.float32
+RECORD_NAMES = ("reward", "cost", "grid", "p2p", "t_in", "action", "index")
+
+
+def price_table(time_f32, grid_cost_avg=cfgmod.GRID_COST_AVG, amplitude=cfgmod.GRID_COST_AMPLITUDE,
+                period=cfgmod.GRID_COST_PERIOD, phase=cfgmod.GRID_COST_PHASE,
+                injection=cfgmod.GRID_INJECTION_PRICE):
+    """GridAgent prices per timestep (agent.py:51-67) and the P2P midpoint (community.py:70).
+
+    Host-side table computed once per environment with TF's f32 constant casting; the device
+    consumes it as an input (SURVEY.md §3.4 item 1 — TF's Eigen sin is not reproducible).
+    """
+    t = np.asarray(time_f32, dtype=F32)
+    freq = F32(2 * np.pi * cfgmod.HOURS_PER_DAY / period)
+    s = np.sin((t * freq) - F32(phase)).astype(F32)
+    buy = ((F32(grid_cost_avg) + F32(amplitude) * s) / F32(cfgmod.CENTS_PER_EURO)).astype(F32)
+    inj = np.full_like(buy, F32(injection))
+    p2p = ((buy + inj) / F32(2)).astype(F32)
+    return buy, inj, p2p
+
+
+class DeviceCommunityBatch:
+    """Device-resident batch of S communities.  All compute runs in libp2pmg.so."""
+
+    def __init__(self, n_scenarios: int, n_agents: int, rounds: int, horizon: int, q_dtype: str = "f64",
+                 device: int = 0, seed: int = 42, scenario_offset: int = 0, **overrides):
+        self.L = _lib.lib()
+        cfg = _lib.default_config()
+        cfg.n_scenarios, cfg.n_agents, cfg.rounds, cfg.horizon = n_scenarios, n_agents, rounds, horizon
+        cfg.q_dtype = _lib.Q_F64 if q_dtype == "f64" else _lib.Q_F32
+        cfg.seed = seed
+        cfg.scenario_offset = scenario_offset
+        for k, v in overrides.items():
+            setattr(cfg, k, v)
+        self.cfg = cfg
+        self.S, self.N, self.R, self.T = n_scenarios, n_agents, rounds, horizon
+        self.A = n_scenarios * n_agents
+        self.q_dtype = q_dtype
+        self.device = device
+        self.seed = seed
+        self.scenario_offset = scenario_offset
+        self.n_states = cfg.n_time_states * cfg.n_temp_states * cfg.n_balance_states * cfg.n_p2p_states
+        self.q_shape = (cfg.n_time_states, cfg.n_temp_states, cfg.n_balance_states, cfg.n_p2p_states,
+                        cfg.n_actions)
+        ctx = C.c_void_p()
+        _lib.check(self.L.p2pmg_create(C.byref(cfg), device, C.byref(ctx)), what="p2pmg_create")
+        self._ctx = ctx
+        self._recorded = 0
+
+    # ----------------------------------------------------------------- lifetime
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            self.L.p2pmg_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def _chk(self, status, what):
+        _lib.check(status, self._ctx, what)
+
+    def sync(self):
+        self._chk(self.L.p2pmg_sync(self._ctx), "sync")
+
+    def device_info(self):
+        buf = C.create_string_buffer(256)
+        mem = C.c_size_t(0)
+        self._chk(self.L.p2pmg_device_info(self._ctx, buf, 256, C.byref(mem)), "device_info")
+        return buf.value.decode(), mem.value
+
+    # ----------------------------------------------------------------- inputs
+    def set_env(self, time, t_out, buy=None, inj=None, p2p=None):
+        """Environment rows (environment.py:26-45): time (slot/96) and outdoor temperature,
+        shape [T] (shared by all scenarios) or [S, T]."""
+        time = np.ascontiguousarray(np.atleast_2d(np.asarray(time, dtype=F32)))
+        t_out = np.ascontiguousarray(np.atleast_2d(np.asarray(t_out, dtype=F32)))
+        if buy is None:
+            buy, inj, p2p = price_table(time)
+        arrs = [np.ascontiguousarray(np.atleast_2d(np.asarray(x, dtype=F32))) for x in (buy, inj, p2p)]
+        n_env = time.shape[0]
+        for x in (time, t_out, *arrs):
+            if x.shape != (n_env, self.T):
+                raise ValueError(f"env arrays must be [{n_env}, {self.T}], got {x.shape}")
+        self._chk(self.L.p2pmg_set_env(self._ctx, n_env, time, t_out, *arrs), "set_env")
+
+    def set_profiles(self, load_w, pv_w):
+        """Per-agent power profiles in W, shape [S, N, T] (community.py:219-224)."""
+        lw = np.ascontiguousarray(np.asarray(load_w, dtype=F32).reshape(self.A, self.T))
+        pw = np.ascontiguousarray(np.asarray(pv_w, dtype=F32).reshape(self.A, self.T))
+        self._chk(self.L.p2pmg_set_profiles(self._ctx, lw, pw), "set_profiles")
+
+    def set_max_in(self, max_in):
+        m = np.ascontiguousarray(np.asarray(max_in, dtype=F32).reshape(self.A))
+        self._chk(self.L.p2pmg_set_agent_params(self._ctx, m), "set_agent_params")
+
+    def set_temperatures(self, t_in, t_m):
+        a = np.ascontiguousarray(np.asarray(t_in, dtype=F32).reshape(self.A))
+        b = np.ascontiguousarray(np.asarray(t_m, dtype=F32).reshape(self.A))
+        self._chk(self.L.p2pmg_set_temperatures(self._ctx, a, b), "set_temperatures")
+
+    def get_temperatures(self):
+        a = np.empty(self.A, F32)
+        b = np.empty(self.A, F32)
+        self._chk(self.L.p2pmg_get_temperatures(self._ctx, a, b), "get_temperatures")
+        return a.reshape(self.S, self.N), b.reshape(self.S, self.N)
+
+    def reset_temperatures_philox(self, episode: int, sigma: float = 0.3):
+        self._chk(self.L.p2pmg_reset_temperatures_philox(self._ctx, int(episode), float(sigma)), "reset_philox")
+
+    def set_replay_codes(self, codes):
+        """uint8 [T, R+1, S, N] (or [T, R+1, N] when S == 1); 255 = greedy."""
+        c = np.ascontiguousarray(np.asarray(codes, dtype=np.uint8).reshape(self.T, self.R + 1, self.A))
+        self._chk(self.L.p2pmg_set_replay_codes(self._ctx, c.ctypes.data), "set_replay_codes")
+
+    # ----------------------------------------------------------------- Q tables
+    def zero_q(self):
+        self._chk(self.L.p2pmg_zero_q(self._ctx), "zero_q")
+
+    def get_q(self, first: int = 0, count: Optional[int] = None, dtype=np.float64):
+        count = self.A - first if count is None else count
+        out = np.empty((count, *self.q_shape), dtype=dtype)
+        code = _lib.Q_F64 if np.dtype(dtype) == np.float64 else _lib.Q_F32
+        self._chk(self.L.p2pmg_get_q(self._ctx, first, count, out.ctypes.data, code), "get_q")
+        return out
+
+    def set_q(self, tables, first: int = 0):
+        t = np.asarray(tables)
+        dtype = np.float64 if t.dtype == np.float64 else np.float32
+        t = np.ascontiguousarray(t.astype(dtype, copy=False).reshape(-1, self.n_states * self.q_shape[-1]))
+        code = _lib.Q_F64 if dtype == np.float64 else _lib.Q_F32
+        self._chk(self.L.p2pmg_set_q(self._ctx, first, t.shape[0], t.ctypes.data, code), "set_q")
+
+    # ----------------------------------------------------------------- the hot path
+    def run_episode(self, mode: str = "train", rng: str = "replay", episode: int = 0, epsilon: float = 0.81,
+                    record: Sequence[str] = ()):
+        """Launch one episode for all scenarios (asynchronous; stream-ordered)."""
+        mask = 0
+        for r in record:
+            mask |= _lib.REC[r]
+        args = _lib.EpisodeArgs(_lib.MODE_TRAIN if mode == "train" else _lib.MODE_GREEDY,
+                                _lib.RNG_REPLAY if rng == "replay" else _lib.RNG_PHILOX,
+                                int(episode), mask, float(epsilon))
+        self._chk(self.L.p2pmg_run_episode(self._ctx, C.byref(args)), "run_episode")
+        self._recorded = mask
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float(0)
+        self._chk(self.L.p2pmg_last_kernel_ms(self._ctx, C.byref(ms)), "last_kernel_ms")
+        return float(ms.value)
+
+    def get_record(self, name: str) -> np.ndarray:
+        """[T, S, N] for per-step records, [T, R+1, S, N] for action/index."""
+        bit = _lib.REC[name]
+        if name in ("action", "index"):
+            shape = (self.T, self.R + 1, self.S, self.N)
+            dt = np.uint8 if name == "action" else np.int32
+        else:
+            shape = (self.T, self.S, self.N)
+            dt = np.float32
+        out = np.empty(shape, dtype=dt)
+        self._chk(self.L.p2pmg_get_record(self._ctx, bit, out.ctypes.data), f"get_record({name})")
+        return out
+
+    def get_records(self, names: Sequence[str]) -> Dict[str, np.ndarray]:
+        return {n: self.get_record(n) for n in names}
+
+    def episode_reward(self) -> np.ndarray:
+        out = np.empty(self.S, F32)
+        self._chk(self.L.p2pmg_get_episode_reward(self._ctx, out), "episode_reward")
+        return out
+
+    # ----------------------------------------------------------------- primitives
+    def rc_step(self, t_out, t_in, t_m, hp):
+        """Batched heating.temperature_simulation (heating.py:37-56) on the device."""
+        arrs = [np.ascontiguousarray(np.asarray(x, dtype=F32).ravel()) for x in np.broadcast_arrays(t_out, t_in, t_m, hp)]
+        n = arrs[0].size
+        a = np.empty(n, F32)
+        b = np.empty(n, F32)
+        self._chk(self.L.p2pmg_rc_step(self._ctx, n, *arrs, a, b), "rc_step")
+        shape = np.broadcast(t_out, t_in, t_m, hp).shape
+        return a.reshape(shape), b.reshape(shape)
+
+    def state_indices(self, obs):
+        """Batched QActor._get_state_indices (rl.py:89-95) on the device; obs [..., 4]."""
+        o = np.ascontiguousarray(np.asarray(obs, dtype=F32).reshape(-1, 4))
+        idx = np.empty(o.shape, np.int32)
+        self._chk(self.L.p2pmg_state_indices(self._ctx, o.shape[0], o, idx.ctypes.data), "state_indices")
+        return idx.reshape(np.shape(obs))
+
+
+def unpack_index(packed: np.ndarray) -> np.ndarray:
+    """P2PMG_REC_INDEX packing -> [..., 4] (it, iT, ib, ip)."""
+    p = np.asarray(packed, dtype=np.int64)
+    return np.stack([p & 0xFF, (p >> 8) & 0xFF, (p >> 16) & 0xFF, (p >> 24) & 0xFF], axis=-1)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# first GPU call: parity tests, then a timing probe if the tests did not crash
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -m gpu -rf > gpurun_out/gpu_tests.log 2>&1
+rc=$?
+echo "pytest exit $rc"
+tail -30 gpurun_out/gpu_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python scripts/quick_timing.py > gpurun_out/quick_timing.log 2>&1
+rc2=$?
+cat gpurun_out/quick_timing.log
+exit $rc2

@@ -1,0 +1,221 @@
+"""GPU parity: the HIP path (libp2pmg.so via its C ABI) against the reference-generated golden
+fixtures and the CPU restatement (oracle/).  Bit-exact for indices, actions and every f32/f64
+value: the kernel and the oracle follow one op order (-ffp-contract=off).
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import philox
+from oracle.restatement import OracleBatch, reference_replay_codes
+from p2pmicrogrid_amd.dataset import scenario_batch
+from p2pmicrogrid_amd.engine import DeviceCommunityBatch, unpack_index
+
+pytestmark = pytest.mark.gpu
+
+LOOPS = ["loop_thesis_T96", "loop_thesis_T672", "loop_homo_T96", "loop_n5_r2_T96"]
+REC = ["reward", "cost", "grid", "p2p", "t_in", "action", "index"]
+
+
+def _engine_from_fixture(d, prefix=""):
+    N, R = int(d["N"]), int(d["R"])
+    T = d[f"{prefix}env_time"].shape[-1]
+    eng = DeviceCommunityBatch(1, N, R, T)
+    eng.set_env(d[f"{prefix}env_time"], d[f"{prefix}env_tout"], d[f"{prefix}buy"], d[f"{prefix}inj"],
+                d[f"{prefix}p2pp"])
+    eng.set_profiles(d[f"{prefix}load_w"][None], d[f"{prefix}pv_w"][None])
+    eng.set_max_in(d["max_in"][None])
+    return eng
+
+
+def test_rc_step_matches_reference_temperature_simulation():
+    d = load_golden("heating")
+    eng = DeviceCommunityBatch(1, 1, 0, 1)
+    a, b = eng.rc_step(d["tout"], d["tin"], d["tm"], d["hp"])
+    assert np.array_equal(a, d["out_in"]) and np.array_equal(b, d["out_m"])
+    for T in (96, 672):
+        hist = d[f"roll{T}_hist"]
+        ti, tm = hist[0, :1].copy(), hist[0, 1:2].copy()
+        for t in range(T):
+            ti, tm = eng.rc_step(d[f"roll{T}_tout"][t:t + 1], ti, tm, d[f"roll{T}_hp"][t:t + 1])
+            assert ti[0] == hist[t + 1, 0] and tm[0] == hist[t + 1, 1], (T, t)
+
+
+def test_state_indices_match_reference_qactor():
+    d = load_golden("qactor")
+    eng = DeviceCommunityBatch(1, 1, 0, 1)
+    idx = eng.state_indices(d["obs"])
+    assert np.array_equal(idx, d["idx"])
+
+
+@pytest.mark.parametrize("name", LOOPS)
+def test_training_replay_matches_reference_loop(name):
+    """Replay mode: exploration replayed from the reference's own np.random consumption."""
+    d = load_golden(name)
+    N, R, E = int(d["N"]), int(d["R"]), int(d["E"])
+    eng = _engine_from_fixture(d)
+    for e in range(E):
+        eng.set_temperatures(d["t_in0"][e][None], d["t_m0"][e][None])
+        eng.set_replay_codes(d["codes"][e])
+        eng.run_episode("train", "replay", episode=e, epsilon=float(d["eps"][e]), record=REC)
+        rec = eng.get_records(REC)
+        for k, g in (("reward", "reward"), ("cost", "cost"), ("grid", "grid"), ("p2p", "p2p"), ("t_in", "t_in")):
+            assert np.array_equal(rec[k][:, 0], d[f"train_{g}"][e]), (name, e, k)
+        assert np.array_equal(rec["action"][:, :, 0], d["train_action"][e]), (name, e)
+        assert np.array_equal(unpack_index(rec["index"][:, :, 0]), d["train_idx"][e]), (name, e)
+        q = eng.get_q()
+        qi, qv = d[f"q_idx_{e}"], d[f"q_val_{e}"]
+        assert np.count_nonzero(q) == len(qv)
+        assert np.array_equal(q[tuple(qi.T)], qv), (name, e)
+    # greedy evaluation (CommunityMicrogrid.run) with the trained tables
+    q = eng.get_q()
+    ev = _engine_from_fixture(d, prefix="eval_")
+    ev.set_q(q)
+    ev.set_temperatures(d["eval_t_in0"][None], d["eval_t_m0"][None])
+    ev.run_episode("greedy", record=REC)
+    rec = ev.get_records(REC)
+    for k in ("reward", "cost", "grid", "p2p", "t_in"):
+        assert np.array_equal(rec[k][:, 0], d[f"eval_{k}"]), (name, "eval", k)
+    assert np.array_equal(rec["action"][:, :, 0], d["eval_action"])
+    assert np.array_equal(unpack_index(rec["index"][:, :, 0]), d["eval_idx"])
+
+
+def _oracle_for(inp, N, R, q_dtype="f64"):
+    S = inp.load_w.shape[0]
+    return OracleBatch(S=S, N=N, R=R, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in,
+                       env_time=inp.time[None], env_tout=inp.t_out, q_dtype=q_dtype)
+
+
+def _device_for(inp, N, R, q_dtype="f64", scenario_offset=0):
+    S, T = inp.load_w.shape[0], inp.load_w.shape[-1]
+    eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, scenario_offset=scenario_offset)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    return eng
+
+
+def _compare(out, rec, tag):
+    for k in ("reward", "cost", "grid", "p2p"):
+        assert np.array_equal(rec[k], out[k]), (tag, k)
+    assert np.array_equal(rec["t_in"], out["t_in"]), tag
+    assert np.array_equal(rec["action"], out["action"].astype(np.uint8)), tag
+    assert np.array_equal(unpack_index(rec["index"]), out["idx"]), tag
+
+
+@pytest.mark.parametrize("N,R,T,q_dtype", [(2, 1, 96, "f64"), (3, 2, 48, "f64"), (5, 0, 40, "f64"),
+                                            (8, 1, 24, "f64"), (16, 1, 12, "f64"), (1, 1, 30, "f64"),
+                                            (2, 1, 96, "f32"), (4, 3, 20, "f32")])
+def test_replay_batch_matches_oracle(N, R, T, q_dtype):
+    """Many scenarios, each with its own RandomState(42 + s) replay stream, several episodes."""
+    S = 64
+    inp = scenario_batch(S, N, T, seed=7)
+    ob = _oracle_for(inp, N, R, q_dtype)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = _device_for(inp, N, R, q_dtype)
+    rss = [np.random.RandomState(42 + s) for s in range(S)]
+    for e, eps in enumerate((0.81, 0.729, 0.2)):
+        codes = np.stack([reference_replay_codes(rs, T, R, N, eps) for rs in rss], axis=2)  # [T,R+1,S,N]
+        eng.set_replay_codes(codes)
+        eng.run_episode("train", "replay", episode=e, epsilon=eps, record=REC)
+        out = ob.run_episode("train", codes=codes, eps=eps)
+        _compare(out, eng.get_records(REC), (N, R, T, q_dtype, e))
+        assert np.array_equal(eng.episode_reward(), out["episode_reward"])
+        a, b = eng.get_temperatures()
+        assert np.array_equal(a, out["t_in_final"]) and np.array_equal(b, out["t_m_final"])
+    q = eng.get_q(dtype=np.float64 if q_dtype == "f64" else np.float32)
+    assert np.array_equal(q.reshape(S * N, -1, 3), ob.q)
+    # greedy pass with the learned tables
+    eng.run_episode("greedy", record=REC)
+    _compare(ob.run_episode("greedy"), eng.get_records(REC), "greedy")
+
+
+def test_philox_matches_oracle_and_t0():
+    S, N, R, T = 256, 2, 1, 96
+    inp = scenario_batch(S, N, T, seed=3)
+    ob = _oracle_for(inp, N, R)
+    eng = _device_for(inp, N, R)
+    for e in range(3):
+        eng.reset_temperatures_philox(e, 0.3)
+        t_in, t_m = philox.t0_draws(42, e, np.arange(S * N))
+        a, b = eng.get_temperatures()
+        assert np.array_equal(a.ravel(), t_in) and np.array_equal(b.ravel(), t_m)
+        ob.t_in, ob.t_m = t_in.reshape(S, N), t_m.reshape(S, N)
+        eps = 0.81 * 0.9 ** e
+        eng.run_episode("train", "philox", episode=e, epsilon=eps, record=REC)
+        out = ob.run_episode("train", rng="philox", seed=42, episode=e, eps=eps)
+        _compare(out, eng.get_records(REC), e)
+    assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
+
+
+def test_full_size_config2_sampled_against_oracle():
+    """configs[1] at full size (4096 scenarios x thesis community): the whole batch runs on the
+    device; 48 sampled scenarios are re-run by the oracle with the same global Philox ids, and
+    size-independent properties are checked over all scenarios."""
+    S, N, R, T = 4096, 2, 1, 96
+    inp = scenario_batch(S, N, T)
+    eng = _device_for(inp, N, R)
+    rng = np.random.RandomState(0)
+    pick = np.sort(rng.choice(S, 48, replace=False))
+    sub = scenario_batch(S, N, T)
+    for k in ("load_w", "pv_w", "max_in", "t_in0", "t_m0", "t_out"):
+        setattr(sub, k, getattr(sub, k)[pick])
+    ob = _oracle_for(sub, N, R)
+    ob.t_in, ob.t_m = sub.t_in0.copy(), sub.t_m0.copy()
+    gids = (pick[:, None] * N + np.arange(N)[None, :])
+    for e in range(2):
+        eng.run_episode("train", "philox", episode=e, epsilon=0.81, record=REC)
+        rec = eng.get_records(REC)
+        out = ob.run_episode("train", rng="philox", seed=42, episode=e, eps=0.81, agent_ids=gids)
+        sl = {k: (v[:, :, pick] if k in ("action", "index") else v[:, pick]) for k, v in rec.items()}
+        _compare(out, sl, e)
+        # properties over ALL scenarios: P2P exchange is antisymmetric (sum_i p2p_i == 0 for N = 2)
+        assert np.all(rec["p2p"].sum(axis=-1) == 0)
+        assert np.all(np.isfinite(rec["reward"])) and np.all(rec["action"] <= 2)
+        # cost identity: cost = ((g*price + p2p*p2p_price) * 15 / 60) * 1e-3 holds elementwise
+    q = eng.get_q(first=0, count=S * N)
+    sel = q.reshape(S, N, -1)[pick].reshape(-1, q[0].size)
+    assert np.array_equal(sel, ob.q.reshape(len(pick) * N, -1))
+
+
+def test_edge_cases_eps_extremes_and_t1():
+    for eps in (0.0, 1.0):
+        S, N, R, T = 32, 2, 1, 24
+        inp = scenario_batch(S, N, T, seed=11)
+        ob = _oracle_for(inp, N, R)
+        ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+        eng = _device_for(inp, N, R)
+        eng.run_episode("train", "philox", episode=0, epsilon=eps, record=REC)
+        _compare(ob.run_episode("train", rng="philox", eps=eps), eng.get_records(REC), eps)
+    # T = 1: the next-step pair wraps onto itself (np.roll(-1) of a single row)
+    inp = scenario_batch(8, 2, 1, seed=5)
+    ob = _oracle_for(inp, 2, 1)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = _device_for(inp, 2, 1)
+    for e in range(3):
+        eng.run_episode("train", "philox", episode=e, epsilon=0.5, record=REC)
+        _compare(ob.run_episode("train", rng="philox", episode=e, eps=0.5), eng.get_records(REC), "T1")
+
+
+def test_q_roundtrip_and_sharded_offsets():
+    S, N, R, T = 40, 2, 1, 16
+    inp = scenario_batch(S, N, T)
+    eng = _device_for(inp, N, R)
+    tab = np.random.RandomState(1).randn(S * N, 20, 20, 20, 20, 3)
+    eng.set_q(tab)
+    assert np.array_equal(eng.get_q(), tab)
+    assert np.array_equal(eng.get_q(first=7, count=5), tab[7:12])
+    # two shards with scenario offsets reproduce the unsharded batch (Philox ids are global)
+    eng.zero_q()
+    eng.run_episode("train", "philox", episode=0, epsilon=0.6, record=REC)
+    full = eng.get_records(REC)
+    parts = []
+    for lo, hi in ((0, 17), (17, 40)):
+        sub = scenario_batch(hi - lo, N, T, first_scenario=lo)
+        e2 = _device_for(sub, N, R, scenario_offset=lo)
+        e2.run_episode("train", "philox", episode=0, epsilon=0.6, record=REC)
+        parts.append(e2.get_records(REC))
+    for k in REC:
+        ax = 2 if k in ("action", "index") else 1
+        assert np.array_equal(np.concatenate([p[k] for p in parts], axis=ax), full[k]), k
