@@ -74,7 +74,7 @@ typedef struct p2pmg_ctx p2pmg_ctx;
 typedef struct p2pmg_config {
   int32_t n_scenarios;      /* S */
   int32_t n_agents;         /* N agents per scenario (1..16) */
-  int32_t rounds;           /* R: negotiation runs R+1 rounds (community.py:75) */
+  int32_t rounds;           /* R: negotiation runs R+1 rounds (community.py:75), R <= 7 */
   int32_t horizon;          /* T timesteps per episode */
   int32_t q_dtype;          /* P2PMG_Q_F64 | P2PMG_Q_F32 */
   int32_t n_time_states;    /* 20 (agent.py:258-261) */
@@ -113,7 +113,15 @@ typedef struct p2pmg_episode_args {
   int32_t episode;  /* episode index (Philox counter) */
   int32_t record;   /* P2PMG_REC_* mask */
   double epsilon;   /* exploration rate shared by every agent (QActor._epsilon) */
+  int32_t flags;    /* P2PMG_FLAG_* (0 = automatic choice) */
+  int32_t reserved;
 } p2pmg_episode_args;
+
+/* Philox placement: a parallel pre-pass writing per-step code words (latency-bound batches:
+ * the episode loop only loads a prefetched word) or inline in the episode kernel (bandwidth-
+ * bound batches: no extra HBM traffic).  Automatic: pre-pass below 2^18 agents.  Same stream. */
+#define P2PMG_FLAG_PHILOX_PREPASS 1
+#define P2PMG_FLAG_PHILOX_INKERNEL 2
 
 /* version / defaults */
 int p2pmg_abi_version(void);

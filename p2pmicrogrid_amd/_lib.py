@@ -48,7 +48,10 @@ class Config(C.Structure):
 
 class EpisodeArgs(C.Structure):
     _fields_ = [("mode", C.c_int32), ("rng", C.c_int32), ("episode", C.c_int32), ("record", C.c_int32),
-                ("epsilon", C.c_double)]
+                ("epsilon", C.c_double), ("flags", C.c_int32), ("reserved", C.c_int32)]
+
+
+FLAG_PHILOX_PREPASS, FLAG_PHILOX_INKERNEL = 1, 2
 
 
 class P2PMGError(RuntimeError):

@@ -10,11 +10,12 @@ constexpr int kEnvStride = 8;  // floats per env row: time, t_out, buy, inj, p2p
 constexpr int kQPad = 4;       // Q row padded to 4 actions: 32-B (f64) / 16-B (f32) aligned rows
 constexpr int kWave = 64;      // one wave per workgroup
 constexpr int kMaxAgents = 16; // compiled-in agents per scenario
+constexpr int kMaxRounds1 = 8; // R + 1 <= 8 (two code words)
 
 // Everything the episode kernel needs, passed by value in the kernarg segment.
 struct EpisodeParams {
   int S, N, R, T, A;
-  int mode, rng, episode, record;
+  int mode, rng, episode, record;  // rng: 0 = code words buffer, 1 = in-kernel Philox
   int n_env;                 // 1 (shared environment) or S (one per scenario)
   const float* env;          // [T][n_env][kEnvStride] time-major
   const float2* prof;        // [T][A] {load_w, pv_w}
@@ -22,7 +23,7 @@ struct EpisodeParams {
   float* t_in;               // [A] in/out
   float* t_m;                // [A] in/out
   void* q;                   // [A][n_states][kQPad] f64 | f32
-  const uint8_t* codes;      // [T][R+1][A] replay codes
+  const uint32_t* codes;     // [T][W][A] code words, W = ceil((R+1)/4), one byte per round (255 = greedy)
   double eps;
   uint32_t seed_lo, seed_hi;
   uint32_t agent_offset;     // global id of local agent 0 (Philox counter)
@@ -47,6 +48,8 @@ struct RcParams {
 };
 
 hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream);
+hipError_t launch_philox_codes(const EpisodeParams& p, uint32_t* words, hipStream_t stream);
+hipError_t launch_pack_codes(int T, int R1, int A, const uint8_t* in, uint32_t* words, hipStream_t stream);
 hipError_t launch_rc_step(int n, const float* t_out, const float* t_in, const float* t_m, const float* hp,
                           float* t_in_new, float* t_m_new, RcParams rc, hipStream_t stream);
 hipError_t launch_state_indices(int n, const float* obs, int32_t* idx, int nt, int nT, int nb, int np,

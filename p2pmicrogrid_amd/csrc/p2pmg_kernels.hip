@@ -19,6 +19,14 @@
 namespace p2pmg {
 namespace {
 
+// x / N for a compile-time N: a multiply by 1/N is bit-identical when N is a power of two
+// (same exact real value, same single rounding), so only other N pay for a division
+template <int N>
+__device__ __forceinline__ float div_n(float x) {
+  if constexpr ((N & (N - 1)) == 0) return x * (1.0f / (float)N);
+  else return x / (float)N;
+}
+
 constexpr int pow2ceil(int n) { return n <= 1 ? 1 : (n <= 2 ? 2 : (n <= 4 ? 4 : (n <= 8 ? 8 : (n <= 16 ? 16 : (n <= 32 ? 32 : 64))))); }
 
 // ----------------------------------------------------------------- reference primitives
@@ -114,22 +122,47 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// xor-shuffle inside a lane group: DPP quad_perm for partners within a quad (a VALU op),
+// ds_bpermute beyond
+template <int D>
+__device__ __forceinline__ float shfl_xor_c(float v) {
+  if constexpr (D == 1) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  } else if constexpr (D == 2) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  } else if constexpr (D == 3) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x1B, 0xF, 0xF, false));  // [3,2,1,0]
+  } else {
+    return __shfl_xor(v, D, 64);
+  }
+}
+
+template <int N, int D>
+__device__ __forceinline__ void exchange_step(const float (&row)[N], float (&col)[N], int i) {
+  const int src = i ^ D;  // partner lane in the group; it sends its row[i]
+  float v = 0.0f;
+#pragma unroll
+  for (int k = 0; k < N; ++k) v = (k == src) ? row[k] : v;  // what my partner wants: row[src]
+  const float got = shfl_xor_c<D>(v);
+#pragma unroll
+  for (int k = 0; k < N; ++k) col[k] = (k == src) ? got : col[k];
+}
+
+template <int N, int D, int G>
+__device__ __forceinline__ void exchange_all(const float (&row)[N], float (&col)[N], int i) {
+  if constexpr (D < G) {
+    exchange_step<N, D>(row, col, i);
+    exchange_all<N, D + 1, G>(row, col, i);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void exchange(const float (&row)[N], float (&col)[N], int i, int sl, float* sh) {
   constexpr int G = pow2ceil(N);
   if constexpr (G <= 8) {
 #pragma unroll
     for (int k = 0; k < N; ++k) col[k] = (k == i) ? row[k] : 0.0f;
-#pragma unroll
-    for (int d = 1; d < G; ++d) {
-      const int src = i ^ d;  // partner lane in the group; it sends its row[i]
-      float v = 0.0f;
-#pragma unroll
-      for (int k = 0; k < N; ++k) v = (k == src) ? row[k] : v;  // what my partner wants: row[partner ^ d] = row[src]
-      const float got = __shfl_xor(v, d, 64);
-#pragma unroll
-      for (int k = 0; k < N; ++k) col[k] = (k == src) ? got : col[k];
-    }
+    exchange_all<N, 1, G>(row, col, i);
   } else {
     if (i < N) {
 #pragma unroll
@@ -149,7 +182,13 @@ template <int N>
 __device__ __forceinline__ float group_sum(float v, int lane, int i, int sl, float* sh) {
   constexpr int G = pow2ceil(N);
   float m = 0.0f;
-  if constexpr (G <= 8) {
+  if constexpr (G == 1) {
+    m = m + v;
+  } else if constexpr (G == 2) {
+    const float o = shfl_xor_c<1>(v);
+    m = m + (i == 0 ? v : o);
+    m = m + (i == 0 ? o : v);
+  } else if constexpr (G <= 8) {
     const int base = lane - i;
 #pragma unroll
     for (int k = 0; k < N; ++k) m = m + __shfl(v, base + k, 64);
@@ -166,50 +205,104 @@ __device__ __forceinline__ float group_sum(float v, int lane, int i, int sl, flo
 struct EnvRow {
   float time, t_out, buy, inj, p2p;
 };
-__device__ __forceinline__ EnvRow load_env(const EpisodeParams& p, int t, int s_env) {
-  const float* e = p.env + ((size_t)t * p.n_env + s_env) * kEnvStride;
-  const float4 a = *reinterpret_cast<const float4*>(e);
-  return EnvRow{a.x, a.y, a.z, a.w, e[4]};
+__device__ __forceinline__ EnvRow load_env(const float* e) {
+  const float4 v = *reinterpret_cast<const float4*>(e);
+  return EnvRow{v.x, v.y, v.z, v.w, e[4]};
 }
 
 // Everything about step t that is known before its negotiation starts.
 struct StepIdx {
-  float bal;        // (load - pv) / max_in           agent.py:172-176
-  int it, iT, ib;   // s indices except p2p          rl.py:89-95
-  size_t strip;     // row of (it, iT, ib, 0)
-  size_t nrow;      // next-state row (time_{t+1}, same T_in, bal_{t+1}, p2p = 0)  agent.py:293-296
+  float bal;        // (load - pv) / max_in of this step    agent.py:172-176
+  float baln;       // ... of the next step (= next step's bal)
+  int it, iT, ib;   // s indices except p2p                 rl.py:89-95
+  uint32_t strip;   // row of (it, iT, ib, 0) in the agent's table
+  uint32_t nrow;    // next-state row (time_{t+1}, same T_in, bal_{t+1}, p2p = 0)  agent.py:293-296
 };
-__device__ __forceinline__ StepIdx make_step(const EpisodeParams& p, float time_t, float time_n, float2 f_t, float2 f_n,
+__device__ __forceinline__ StepIdx make_step(const EpisodeParams& p, float time_t, float time_n, float bal, float2 f_n,
                                              float tin, float mi, int ip_zero) {
   StepIdx st;
-  st.bal = (f_t.x - f_t.y) / mi;
-  const float baln = (f_n.x - f_n.y) / mi;
-  const float tnorm = (tin - p.setpoint) / p.margin;  // heating.py:118-120
+  st.bal = bal;
+  st.baln = (f_n.x - f_n.y) / mi;
+  const float dt = tin - p.setpoint;  // heating.py:118-120 (x / 1.0 == x exactly)
+  const float tnorm = p.margin == 1.0f ? dt : dt / p.margin;
   st.it = idx_time(time_t, p.nt);
   st.iT = idx_temp(tnorm, p.nT);
-  st.ib = idx_plain(st.bal, p.nb);
-  st.strip = (((size_t)st.it * p.nT + st.iT) * p.nb + st.ib) * p.np;
+  st.ib = idx_plain(bal, p.nb);
+  st.strip = (uint32_t)(((st.it * p.nT + st.iT) * p.nb + st.ib) * p.np);
   const int itn = idx_time(time_n, p.nt);
-  const int ibn = idx_plain(baln, p.nb);
-  st.nrow = (((size_t)itn * p.nT + st.iT) * p.nb + ibn) * p.np + ip_zero;
+  const int ibn = idx_plain(st.baln, p.nb);
+  st.nrow = (uint32_t)(((itn * p.nT + st.iT) * p.nb + ibn) * p.np + ip_zero);
   return st;
 }
 
-// exploration code for (t, r): 255 = greedy (QActor.select_action rl.py:100-111)
-__device__ __forceinline__ int decision_code(const EpisodeParams& p, int t, int r, int a, bool active) {
-  if (p.mode != 0 || !active) return 255;
-  const int R1 = p.R + 1;
-  if (p.rng == 0) return p.codes[((size_t)t * R1 + r) * p.A + a];
-  uint32_t c0 = (uint32_t)(t * R1 + r), c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a, c3 = kTagDecision;
+// Philox exploration draw for (t, r): 255 = greedy (QActor.select_action rl.py:100-111)
+__device__ __forceinline__ uint32_t philox_code(const EpisodeParams& p, int t, int r, uint32_t gid) {
+  uint32_t c0 = (uint32_t)(t * (p.R + 1) + r), c1 = (uint32_t)p.episode, c2 = gid, c3 = kTagDecision;
   philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
   const double u = ((double)(c0 >> 5) * 67108864.0 + (double)(c1 >> 6)) / 9007199254740992.0;
-  return u < p.eps ? (int)(((uint64_t)c2 * 3ull) >> 32) : 255;
+  return u < p.eps ? (uint32_t)(((uint64_t)c2 * 3ull) >> 32) : 255u;
+}
+
+// all rounds' codes of step t packed one byte per round (round r in bits 8r..8r+7)
+// The code-word buffer always exists (greedy runs read and ignore it), so the loads are
+// unconditional and branch-free: a load whose destination is touched under a branch before
+// its use is waited for at that branch.  The in-kernel Philox words are built separately.
+struct CodeWords {
+  uint32_t w0, w1;  // loaded words
+  uint64_t gen;     // in-kernel Philox word (p.rng == 1)
+};
+__device__ __forceinline__ CodeWords step_codes(const EpisodeParams& p, int t, int a) {
+  const int R1 = p.R + 1;
+  const int W = (R1 + 3) >> 2;  // code words [T][W][A] (replay upload or Philox pre-pass)
+  const size_t k0 = ((size_t)t * W) * p.A + a;
+  CodeWords c;
+  c.w0 = p.codes[k0];
+  c.w1 = p.codes[W > 1 ? k0 + p.A : k0];
+  c.gen = ~0ull;
+  if (p.rng == 1) {
+    for (int r = 0; r < R1; ++r) {
+      const uint64_t v = philox_code(p, t, r, p.agent_offset + (uint32_t)a);
+      c.gen = (c.gen & ~(0xFFull << (8 * r))) | (v << (8 * r));
+    }
+  }
+  return c;
+}
+__device__ __forceinline__ uint64_t code_word(const EpisodeParams& p, const CodeWords& c, bool active) {
+  const int R1 = p.R + 1;
+  uint64_t w = (uint64_t)c.w0 | ((R1 > 4 ? (uint64_t)c.w1 : 0xFFFFFFFFull) << 32);
+  w |= (R1 < 8 ? ~0ull << (8 * R1) : 0ull);
+  if (p.rng == 1) w = c.gen;
+  return (p.mode != 0 || !active) ? ~0ull : w;
+}
+
+// A TD store can hit a row whose prefetch was issued before it.  The prefetched registers
+// are not touched (that would force a wait for the load); the patch is applied at use.
+template <typename QT>
+struct Patch {
+  uint32_t row;  // 0xFFFFFFFF = none
+  int act;
+  QT val;
+};
+template <typename QT>
+__device__ __forceinline__ Row4<QT> patched(Row4<QT> r, uint32_t addr, const Patch<QT>& pt) {
+  if (pt.row == addr) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r.v[k] = (pt.act == k) ? pt.val : r.v[k];
+  }
+  return r;
+}
+
+// heat-pump power of an action without a dynamically indexed kernarg array (that compiles to
+// a global load + vmcnt(0) on the critical path)
+__device__ __forceinline__ float hp_of(const EpisodeParams& p, int act) {
+  const float l0 = p.hp_levels[0], l1 = p.hp_levels[1], l2 = p.hp_levels[2];
+  return act == 0 ? l0 : (act == 1 ? l1 : l2);
 }
 
 // ----------------------------------------------------------------- the episode kernel
 // One launch = one episode of T timesteps for every scenario (train_episode / run).
 // Latency structure per step (one dependent Q gather per extra round):
-//   * env rows and profiles are prefetched two steps ahead;
+//   * env rows, profiles and exploration codes are prefetched ahead;
 //   * round 0 always sees P = 0, so its p2p index is the constant ip_zero and its Q row, like
 //     the next-state row, is known as soon as the previous step's final action is: both are
 //     issued right after that action, before the previous step's market/reward/TD work;
@@ -232,32 +325,53 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   const int T = p.T;
   const int R1 = p.R + 1;
   const bool train = p.mode == 0;
+  const size_t A = (size_t)p.A;
 
-  const size_t n_states = (size_t)p.nt * p.nT * p.nb * p.np;
+  const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
   QT* __restrict__ q = reinterpret_cast<QT*>(p.q) + (size_t)a * n_states * kQPad;
   const float mi = active ? p.max_in[a] : 1.0f;
   float tin = active ? p.t_in[a] : p.setpoint;
   float tm = active ? p.t_m[a] : p.setpoint;
   // round 0 and the next state both have p2p = mean(-0 ... -0) / max_in = 0 (agent.py:203, community.py:161)
-  const int ip_zero = idx_plain((0.0f / (float)N) / mi, p.np);
+  const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, p.np);
 
-  auto wrap = [T](int t) { return t % T; };  // np.roll(-1) pairing (dataset.py:101)
-  auto prof = [&](int t) { return active ? p.prof[(size_t)t * p.A + a] : make_float2(0.0f, 0.0f); };
+  // running offsets (no 64-bit multiplies in the loop)
+  const float* envb = p.env + (size_t)s_env * kEnvStride;
+  const size_t env_step = (size_t)p.n_env * kEnvStride;
+  const size_t env_end = env_step * T;
+  const float2* profb = p.prof + a;
+  const size_t prof_end = A * T;
+  auto prof_at = [&](size_t off) { return profb[off]; };  // inactive lanes read agent 0 (a = 0)
+  auto adv = [](size_t off, size_t step, size_t end) { off += step; return off >= end ? off - end : off; };
+  size_t e1o = adv(0, env_step, env_end), e2o = adv(e1o, env_step, env_end);
+  size_t f1o = adv(0, A, prof_end), f2o = adv(f1o, A, prof_end);
 
-  EnvRow e0 = load_env(p, 0, s_env);
-  EnvRow e1 = load_env(p, wrap(1), s_env);
-  float2 f0 = prof(0), f1 = prof(wrap(1));
-  StepIdx st = make_step(p, e0.time, e1.time, f0, f1, tin, mi, ip_zero);
-  int code0 = decision_code(p, 0, 0, a, active);
-  const Row4<QT> zrow{{(QT)0, (QT)0, (QT)0, (QT)0}};
-  Row4<QT> row0 = (active && code0 == 255) ? load_row(q + (st.strip + ip_zero) * kQPad) : zrow;
-  Row4<QT> rowN = (active && train) ? load_row(q + st.nrow * kQPad) : zrow;
+  EnvRow e0 = load_env(envb);
+  EnvRow e1 = load_env(envb + e1o);
+  const float2 f0 = prof_at(0);
+  float2 f1 = prof_at(f1o);
+  StepIdx st = make_step(p, e0.time, e1.time, (f0.x - f0.y) / mi, f1, tin, mi, ip_zero);
+  uint64_t cw = code_word(p, step_codes(p, 0, a), active);
+  // Q rows are loaded unconditionally (a load under a divergent branch is waited for at the
+  // join, which would serialise the prefetch); a row that is not needed aliases one that is
+  // loaded anyway, so it costs no HBM traffic.  Inactive lanes read agent 0's table.
+  auto row0_addr = [&](const StepIdx& x, uint64_t c) -> uint32_t {
+    const bool need = ((c & 0xFF) == 255) || (train && R1 == 1);  // greedy, or the TD target itself
+    return need ? x.strip + (uint32_t)ip_zero : x.nrow;
+  };
+  uint32_t a0 = row0_addr(st, cw);
+  uint32_t aN = train ? st.nrow : a0;
+  Row4<QT> row0 = load_row(q + a0 * kQPad);
+  Row4<QT> rowN = load_row(q + aN * kQPad);
+  Patch<QT> pat{0xFFFFFFFFu, 0, (QT)0};
   float ep_sum = 0.0f;
+  size_t tA = 0;
 
-  for (int t = 0; t < T; ++t) {
-    // prefetch two steps ahead
-    const EnvRow e2 = load_env(p, wrap(t + 2), s_env);
-    const float2 f2 = prof(wrap(t + 2));
+  for (int t = 0; t < T; ++t, tA += A) {
+    // prefetch ahead: env/profile two steps, exploration codes one step
+    const EnvRow e2 = load_env(envb + e2o);
+    const float2 f2 = prof_at(f2o);
+    const CodeWords cw1r = step_codes(p, t + 1 == T ? 0 : t + 1, a);
 
     float row[N];
     float col[N];
@@ -265,25 +379,25 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
     for (int j = 0; j < N; ++j) { row[j] = 0.0f; col[j] = 0.0f; }
     int act = 0, ip = ip_zero;
     float hp = 0.0f;
+    row0 = patched(row0, a0, pat);  // the previous step's TD store may have hit a prefetched row
+    rowN = patched(rowN, aN, pat);
     Row4<QT> rowR = row0;  // Q row of the final round's state (TD target Q[s, a])
 
     for (int r = 0; r < R1; ++r) {
-      int code;
-      if (r == 0) {
-        code = code0;
-      } else {
+      const int code = (int)((cw >> (8 * r)) & 0xFF);
+      if (r > 0) {
         exchange<N>(row, col, i, sl, shP);  // Jacobi: read the previous round's column (community.py:84-86)
         // powers = -P[:, i] with the diagonal zeroed (community.py:76,81); p2p = mean / max_in (agent.py:203)
         float acc = 0.0f;
 #pragma unroll
         for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : col[j]));
-        ip = idx_plain((acc / (float)N) / mi, p.np);
-        code = decision_code(p, t, r, a, active);
+        ip = idx_plain(div_n<N>(acc) / mi, p.np);
         // the final round's row is needed for the TD update even when exploring
-        if (active && (code == 255 || (train && r == R1 - 1))) rowR = load_row(q + (st.strip + ip) * kQPad);
+        const bool need = code == 255 || (train && r == R1 - 1);
+        rowR = load_row(q + (need ? st.strip + (uint32_t)ip : a0) * kQPad);
       }
       act = code == 255 ? argmax3(rowR) : code;  // QAgent._act / take_decision (agent.py:271-289)
-      hp = p.hp_levels[act];
+      hp = hp_of(p, act);
 
       // RLAgent._divide_power agent.py:186-195 on out = bal * max_in + hp (agent.py:210)
       const float out = (st.bal * mi) + hp;
@@ -298,7 +412,7 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
       }
       tot = fabsf(tot);
       if (tot == 0.0f) {
-        const float ev = (out * 1.0f) / (float)N;
+        const float ev = div_n<N>(out * 1.0f);
 #pragma unroll
         for (int j = 0; j < N; ++j) row[j] = ev;
       } else {
@@ -306,26 +420,24 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
         for (int j = 0; j < N; ++j) row[j] = (out * fabsf(f[j])) / tot;
       }
       if (active) {
-        const size_t k = ((size_t)t * R1 + r) * p.A + a;
+        const size_t k = (tA * R1) + (size_t)r * A + a;
         if (p.record & 32) p.rec_action[k] = (uint8_t)act;
         if (p.record & 64) p.rec_index[k] = st.it | (st.iT << 8) | (st.ib << 16) | (ip << 24);
       }
     }
-    if (train && active && R1 == 1 && code0 != 255) rowR = load_row(q + (st.strip + ip) * kQPad);
 
     // CommunityMicrogrid._step -> HPHeating.step (community.py:184-188, heating.py:138-143):
     // computed now so the next step's rows can be issued before this step's market work
     float tin1 = tin, tm1 = tm;
     rc_update(p, e0.t_out, hp, tin1, tm1);
-    StepIdx st1 = st;
-    int code1 = 255;
-    Row4<QT> row0n = zrow, rowNn = zrow;
-    if (t + 1 < T) {
-      st1 = make_step(p, e1.time, e2.time, f1, f2, tin1, mi, ip_zero);
-      code1 = decision_code(p, t + 1, 0, a, active);
-      if (active && code1 == 255) row0n = load_row(q + (st1.strip + ip_zero) * kQPad);
-      if (active && train) rowNn = load_row(q + st1.nrow * kQPad);
-    }
+    // (after the last step this prefetches a wrapped, unused step: harmless valid addresses)
+    const StepIdx st1 = make_step(p, e1.time, e2.time, st.baln, f2, tin1, mi, ip_zero);
+    const uint64_t cw1 = code_word(p, cw1r, active);
+    const uint32_t a0n = row0_addr(st1, cw1);
+    const uint32_t aNn = train ? st1.nrow : a0n;
+    const Row4<QT> row0n = load_row(q + a0n * kQPad);
+    const Row4<QT> rowNn = load_row(q + aNn * kQPad);
+    pat.row = 0xFFFFFFFFu;
 
     // CommunityMicrogrid._assign_powers community.py:45-54 on the final P (diagonal kept)
     exchange<N>(row, col, i, sl, shP);
@@ -350,15 +462,13 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
 
     if (train && active) {
       // QAgent.train agent.py:293-298 -> QActor.train rl.py:119-129
-      const size_t srow = st.strip + ip;
+      const uint32_t srow = st.strip + ip;
       const QT qnew = td_update(rowR.v[act], rw, max3(rowN), p.alpha, p.gamma);
       q[srow * kQPad + act] = qnew;
-      // rows issued before this store see the old value: patch the register copies
-      if (st1.strip + ip_zero == srow) row0n.v[act] = qnew;
-      if (st1.nrow == srow) rowNn.v[act] = qnew;
+      pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
     }
     if (active) {
-      const size_t k = (size_t)t * p.A + a;
+      const size_t k = tA + a;
       if (p.record & 1) p.rec_reward[k] = rw;
       if (p.record & 2) p.rec_cost[k] = cost;
       if (p.record & 4) p.rec_grid[k] = g;
@@ -367,16 +477,19 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
     }
     // avg_reward = sum_t mean_i r (community.py:179), canonical sequential order
     const float m = group_sum<N>(rw, lane, i, sl, shR);
-    ep_sum = ep_sum + m / (float)N;
+    ep_sum = ep_sum + div_n<N>(m);
 
     tin = tin1;
     tm = tm1;
     e0 = e1;
     e1 = e2;
-    f0 = f1;
     f1 = f2;
+    e2o = adv(e2o, env_step, env_end);
+    f2o = adv(f2o, A, prof_end);
     st = st1;
-    code0 = code1;
+    cw = cw1;
+    a0 = a0n;
+    aN = aNn;
     row0 = row0n;
     rowN = rowNn;
   }
@@ -384,6 +497,39 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
     p.t_in[a] = tin;
     p.t_m[a] = tm;
     if (i == 0) p.ep_reward[s] = ep_sum;
+  }
+}
+
+// Philox pre-pass: every (t, agent) code word of an episode in one parallel launch, so the
+// latency-bound episode loop only loads a prefetched word instead of computing R+1 blocks.
+__global__ void philox_codes_kernel(const EpisodeParams p, uint32_t* __restrict__ words) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
+  if (k >= (size_t)p.T * p.A) return;
+  const int t = (int)(k / p.A), a = (int)(k % p.A);
+  const int R1 = p.R + 1, W = (R1 + 3) >> 2;
+  for (int w = 0; w < W; ++w) {
+    uint32_t word = 0xFFFFFFFFu;
+    for (int b = 0; b < 4 && 4 * w + b < R1; ++b) {
+      const uint32_t c = philox_code(p, t, 4 * w + b, p.agent_offset + (uint32_t)a);
+      word = (word & ~(0xFFu << (8 * b))) | (c << (8 * b));
+    }
+    words[((size_t)t * W + w) * p.A + a] = word;
+  }
+}
+
+// host replay codes u8 [T][R1][A] -> code words [T][W][A]
+__global__ void pack_codes_kernel(int T, int R1, int A, const uint8_t* __restrict__ in, uint32_t* __restrict__ words) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (size_t)T * A) return;
+  const int t = (int)(k / A), a = (int)(k % A);
+  const int W = (R1 + 3) >> 2;
+  for (int w = 0; w < W; ++w) {
+    uint32_t word = 0xFFFFFFFFu;
+    for (int b = 0; b < 4 && 4 * w + b < R1; ++b) {
+      const uint32_t c = in[((size_t)t * R1 + 4 * w + b) * A + a];
+      word = (word & ~(0xFFu << (8 * b))) | (c << (8 * b));
+    }
+    words[((size_t)t * W + w) * A + a] = word;
   }
 }
 
@@ -471,6 +617,20 @@ __global__ void prof_pack_kernel(int A, int T, const float* load_w, const float*
 inline unsigned grid_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
+
+hipError_t launch_philox_codes(const EpisodeParams& p, uint32_t* words, hipStream_t stream) {
+  const size_t n = (size_t)p.T * p.A;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(philox_codes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, p, words);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_codes(int T, int R1, int A, const uint8_t* in, uint32_t* words, hipStream_t stream) {
+  const size_t n = (size_t)T * A;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_codes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, T, R1, A, in, words);
+  return hipGetLastError();
+}
 
 hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream) {
   return q_dtype == 0 ? launch_q<double>(p, stream) : launch_q<float>(p, stream);

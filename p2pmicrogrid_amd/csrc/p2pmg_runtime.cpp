@@ -35,7 +35,8 @@ struct p2pmg_ctx {
   float* t_in = nullptr;
   float* t_m = nullptr;
   void* q = nullptr;
-  uint8_t* codes = nullptr;
+  uint32_t* codes = nullptr;  // code words [T][W][A]
+  int code_src = 0;          // what the code buffer holds: 0 none, 1 replay upload, 2 Philox pre-pass
   float* ep_reward = nullptr;
   float* rec_f32[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // reward, cost, grid, p2p, tin
   uint8_t* rec_action = nullptr;
@@ -140,6 +141,7 @@ int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
   if (!cfg || !out) return P2PMG_E_INVALID;
   *out = nullptr;
   if (cfg->n_scenarios <= 0 || cfg->n_agents <= 0 || cfg->rounds < 0 || cfg->horizon <= 0) return P2PMG_E_INVALID;
+  if (cfg->rounds + 1 > p2pmg::kMaxRounds1) return P2PMG_E_UNSUPPORTED;
   if (cfg->n_actions != 3) return P2PMG_E_UNSUPPORTED;
   const int N = cfg->n_agents;
   if (!((N >= 1 && N <= 8) || N == 16)) return P2PMG_E_UNSUPPORTED;
@@ -168,6 +170,11 @@ int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
       dmalloc(&c->t_in, A) != hipSuccess || dmalloc(&c->t_m, A) != hipSuccess ||
       dmalloc(&c->ep_reward, (size_t)c->S) != hipSuccess)
     return bail(P2PMG_E_NOMEM);
+  // the code-word buffer always exists: greedy episodes read (and ignore) it, which keeps the
+  // kernel's code loads unconditional
+  const size_t ncw = (size_t)c->T * ((c->R + 4) / 4) * A;
+  if (dmalloc(&c->codes, ncw) != hipSuccess) return bail(P2PMG_E_NOMEM);
+  if (hipMemsetAsync(c->codes, 0xFF, ncw * 4, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
   const size_t qbytes = A * c->n_states * kQPad * c->q_elem;
   if (hipMalloc(&c->q, qbytes) != hipSuccess) return bail(P2PMG_E_NOMEM);
   if (hipMemsetAsync(c->q, 0, qbytes, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
@@ -300,13 +307,25 @@ int p2pmg_reset_temperatures_philox(p2pmg_ctx* c, int episode, double sigma) {
   return P2PMG_OK;
 }
 
+static int ensure_codes(p2pmg_ctx* c) {
+  if (!c->codes) HIP_TRY(c, dmalloc(&c->codes, (size_t)c->T * ((c->R + 4) / 4) * c->A));
+  return P2PMG_OK;
+}
+
 int p2pmg_set_replay_codes(p2pmg_ctx* c, const uint8_t* codes) {
   if (!c || !codes) return P2PMG_E_INVALID;
   const size_t n = (size_t)c->T * (c->R + 1) * c->A;
-  if (!c->codes) HIP_TRY(c, dmalloc(&c->codes, n));
-  HIP_TRY(c, hipMemcpyAsync(c->codes, codes, n, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  int rc = ensure_codes(c);
+  if (rc != P2PMG_OK) return rc;
+  uint8_t* staging = nullptr;
+  HIP_TRY(c, dmalloc(&staging, n));
+  hipError_t e = hipMemcpyAsync(staging, codes, n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = p2pmg::launch_pack_codes(c->T, c->R + 1, c->A, staging, c->codes, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(staging);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("set_replay_codes: ") + hipGetErrorString(e));
   c->have_codes = true;
+  c->code_src = 1;
   return P2PMG_OK;
 }
 
@@ -371,7 +390,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   p.T = c->T;
   p.A = c->A;
   p.mode = args->mode;
-  p.rng = args->rng;
+  p.rng = 0;
   p.episode = args->episode;
   p.record = args->record;
   p.n_env = c->n_env;
@@ -383,6 +402,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   p.q = c->q;
   p.codes = c->codes;
   p.eps = args->epsilon;
+  if (train && args->rng == P2PMG_RNG_PHILOX) p.rng = 1;  // in-kernel unless the pre-pass below runs
   p.seed_lo = (uint32_t)(g.seed & 0xFFFFFFFFu);
   p.seed_hi = (uint32_t)(g.seed >> 32);
   p.agent_offset = (uint32_t)(g.scenario_offset * c->N);
@@ -419,6 +439,20 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   p.mph = g.minutes_per_hour;
   p.kilo = g.kilo;
   p.penw = g.penalty_weight;
+  if (train && args->rng == P2PMG_RNG_PHILOX) {
+    bool prepass = c->A < (1 << 18);
+    if (args->flags & P2PMG_FLAG_PHILOX_PREPASS) prepass = true;
+    if (args->flags & P2PMG_FLAG_PHILOX_INKERNEL) prepass = false;
+    if (prepass) {
+      rc = ensure_codes(c);
+      if (rc != P2PMG_OK) return rc;
+      p.codes = c->codes;
+      HIP_TRY(c, p2pmg::launch_philox_codes(p, c->codes, c->stream));
+      c->code_src = 2;
+      c->have_codes = false;  // a replay upload must be repeated after a pre-pass overwrote it
+      p.rng = 0;
+    }
+  }
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
   hipError_t e = p2pmg::launch_episode(p, g.q_dtype, c->stream);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));

@@ -153,14 +153,16 @@ class DeviceCommunityBatch:
 
     # ----------------------------------------------------------------- the hot path
     def run_episode(self, mode: str = "train", rng: str = "replay", episode: int = 0, epsilon: float = 0.81,
-                    record: Sequence[str] = ()):
-        """Launch one episode for all scenarios (asynchronous; stream-ordered)."""
+                    record: Sequence[str] = (), philox: str = "auto"):
+        """Launch one episode for all scenarios (asynchronous; stream-ordered).
+        philox: 'auto' | 'prepass' | 'inkernel' placement of the Philox draws."""
         mask = 0
         for r in record:
             mask |= _lib.REC[r]
+        flags = {"auto": 0, "prepass": _lib.FLAG_PHILOX_PREPASS, "inkernel": _lib.FLAG_PHILOX_INKERNEL}[philox]
         args = _lib.EpisodeArgs(_lib.MODE_TRAIN if mode == "train" else _lib.MODE_GREEDY,
                                 _lib.RNG_REPLAY if rng == "replay" else _lib.RNG_PHILOX,
-                                int(episode), mask, float(epsilon))
+                                int(episode), mask, float(epsilon), flags, 0)
         self._chk(self.L.p2pmg_run_episode(self._ctx, C.byref(args)), "run_episode")
         self._recorded = mask
 

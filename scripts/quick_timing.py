@@ -6,7 +6,7 @@ from p2pmicrogrid_amd.dataset import scenario_batch
 from p2pmicrogrid_amd.engine import DeviceCommunityBatch
 
 for q_dtype in ("f64", "f32"):
-    for S in ((4096, 16384) if q_dtype == "f64" else (4096, 16384, 65536)):
+    for S in (4096, 16384):
         N, R, T = 2, 1, 96
         inp = scenario_batch(S, N, T)
         eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype)

@@ -106,7 +106,8 @@ def _compare(out, rec, tag):
 
 @pytest.mark.parametrize("N,R,T,q_dtype", [(2, 1, 96, "f64"), (3, 2, 48, "f64"), (5, 0, 40, "f64"),
                                             (8, 1, 24, "f64"), (16, 1, 12, "f64"), (1, 1, 30, "f64"),
-                                            (2, 1, 96, "f32"), (4, 3, 20, "f32")])
+                                            (2, 1, 96, "f32"), (4, 3, 20, "f32"), (2, 7, 10, "f64"),
+                                            (6, 4, 10, "f32")])
 def test_replay_batch_matches_oracle(N, R, T, q_dtype):
     """Many scenarios, each with its own RandomState(42 + s) replay stream, several episodes."""
     S = 64
@@ -131,7 +132,8 @@ def test_replay_batch_matches_oracle(N, R, T, q_dtype):
     _compare(ob.run_episode("greedy"), eng.get_records(REC), "greedy")
 
 
-def test_philox_matches_oracle_and_t0():
+@pytest.mark.parametrize("placement", ["prepass", "inkernel"])
+def test_philox_matches_oracle_and_t0(placement):
     S, N, R, T = 256, 2, 1, 96
     inp = scenario_batch(S, N, T, seed=3)
     ob = _oracle_for(inp, N, R)
@@ -143,7 +145,7 @@ def test_philox_matches_oracle_and_t0():
         assert np.array_equal(a.ravel(), t_in) and np.array_equal(b.ravel(), t_m)
         ob.t_in, ob.t_m = t_in.reshape(S, N), t_m.reshape(S, N)
         eps = 0.81 * 0.9 ** e
-        eng.run_episode("train", "philox", episode=e, epsilon=eps, record=REC)
+        eng.run_episode("train", "philox", episode=e, epsilon=eps, record=REC, philox=placement)
         out = ob.run_episode("train", rng="philox", seed=42, episode=e, eps=eps)
         _compare(out, eng.get_records(REC), e)
     assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
@@ -173,7 +175,6 @@ def test_full_size_config2_sampled_against_oracle():
         # properties over ALL scenarios: P2P exchange is antisymmetric (sum_i p2p_i == 0 for N = 2)
         assert np.all(rec["p2p"].sum(axis=-1) == 0)
         assert np.all(np.isfinite(rec["reward"])) and np.all(rec["action"] <= 2)
-        # cost identity: cost = ((g*price + p2p*p2p_price) * 15 / 60) * 1e-3 holds elementwise
     q = eng.get_q(first=0, count=S * N)
     sel = q.reshape(S, N, -1)[pick].reshape(-1, q[0].size)
     assert np.array_equal(sel, ob.q.reshape(len(pick) * N, -1))
