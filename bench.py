@@ -1,0 +1,208 @@
+#!/usr/bin/env python
+"""bench.py — agent-steps/s of the P2PMicrogrid hot path on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 4096 independent scenarios x the reference thesis community
+(N = 2 PV + heat-pump households, R = 1 -> 2 negotiation rounds, T = 96 quarter-hour slots per
+episode, heterogeneous ratings/T0, per-agent float64 Q-tables, epsilon-greedy tabular Q-learning
+with the reference's epsilon schedule).  One bench "step" = one training episode
+(CommunityMicrogrid.train_episode, community.py:149-182) for every scenario of the rank:
+T0 reset (heating.py:145-152) + exploration draws + the fused episode kernel.  Data are
+synthetic profiles with the reference schema (the SQLite source is not available).
+
+N GPUs: one process per GPU (torchrun), scenarios sharded with no data-path collective (each
+scenario's tables are private: "replicas only"); torch.distributed(gloo) carries only the
+barrier and the max-over-ranks time.  value = all ranks' agent-steps / max time (weak scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "agent-steps/sec (whole node, rollout+Q-update) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes_per_agent_step(R: int, q_bytes: int, outputs: int = 2) -> int:
+    """8 (load_w, pv_w) + q_bytes * (3(R+1) + 3 + 2) (greedy gathers per round,
+    next-state max, Q[s,a] read+write) + 4 * outputs (reward, cost).  The persistent variant keeps
+    T_in/T_m in registers for the whole episode, so the 16 B of state traffic is dropped."""
+    return 8 + q_bytes * (3 * (R + 1) + 3 + 2) + 4 * outputs
+
+
+def epsilon_at(episode: int, eps0: float = 0.81, decay: float = 0.9, every: int = 50, floor: float = 0.1) -> float:
+    """community.py:279-286 + rl.py:131-132: decay after episodes 0, 50, 100, ... (floor 0.1)."""
+    n = 0 if episode == 0 else (episode - 1) // every + 1
+    eps = eps0
+    for _ in range(n):
+        eps = max(floor, decay * eps)
+    return eps
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist  # gloo: barrier + max-time only, no GPU interaction
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 96):
+    """The oracle (NumPy CPU restatement, oracle/restatement.py) on a bounded sample of the same
+    workload, single-threaded, Philox exploration."""
+    from oracle.restatement import OracleBatch
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    inp = scenario_batch(S, N, T)
+    ob = OracleBatch(S=S, N=N, R=R, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in,
+                     env_time=inp.time[None], env_tout=inp.t_out)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    t0 = time.perf_counter()
+    eps_done = 0
+    while True:
+        ob.run_episode("train", rng="philox", episode=eps_done, eps=epsilon_at(eps_done))
+        eps_done += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": S * N * T * eps_done / dt, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{S} scenarios x thesis community (N={N}, R={R}, T={T}), {eps_done} training episodes, "
+                      f"oracle/restatement.py vectorised NumPy, {dt:.1f} s"}
+
+
+def load_traffic(path: str, workload: str):
+    """HBM bytes per episode-kernel launch from a committed rocprofv3 PMC summary (or None)."""
+    if not path or not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+    except Exception:  # noqa: BLE001
+        return None
+    if d.get("workload") != workload:
+        return None
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50, help="timed episodes")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed episodes")
+    ap.add_argument("--scenarios", type=int, default=4096, help="scenarios per GPU (configs[1]: 4096)")
+    ap.add_argument("--agents", type=int, default=2)
+    ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--horizon", type=int, default=96)
+    ap.add_argument("--q-dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    rank, world, local = dist_setup()
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    from p2pmicrogrid_amd.engine import DeviceCommunityBatch
+
+    S, N, R, T = args.scenarios, args.agents, args.rounds, args.horizon
+    first = rank * S
+    inp = scenario_batch(S, N, T, first_scenario=first)
+    eng = DeviceCommunityBatch(S, N, R, T, q_dtype=args.q_dtype, device=local, scenario_offset=first)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    record = ("reward", "cost")
+
+    def episode(e):
+        eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record)
+        eng.reset_temperatures_philox(e + 1, 0.3)  # agent.reset() at the end of train_episode
+
+    for e in range(args.warmup):
+        episode(e)
+    eng.sync()
+    eng.reset_kernel_times()
+    barrier(world)
+    eng.sync()
+    t0 = time.perf_counter()
+    for e in range(args.warmup, args.warmup + args.steps):
+        episode(e)
+    eng.sync()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    dt = max_over_ranks(dt, world)
+    kms = eng.kernel_times()
+    ep_reward = float(np.mean(eng.episode_reward()))
+
+    steps_per_episode = S * N * T
+    value = world * steps_per_episode * args.steps / dt
+    q_bytes = 8 if args.q_dtype == "f64" else 4
+    bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
+    kernel_ms = float(np.mean(kms)) if len(kms) else float("nan")
+    achieved = bpa * steps_per_episode / (kernel_ms * 1e-3) / 1e9
+    workload = (f"configs[1]: {S} scenarios/GPU x thesis community (N={N}, R={R}, T={T}), per-agent "
+                f"{args.q_dtype} Q-tables, Philox exploration, train episodes")
+    traffic = load_traffic(args.traffic_json, workload)
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 simulation, f64 Q-table" if args.q_dtype == "f64" else "f32",
+            "data": "synthetic profiles with the reference dataset schema (seed 42)",
+            "config": {"workload": workload, "scenarios_per_gpu": S, "agents_per_scenario": N,
+                       "rounds": R + 1, "horizon": T, "q_dtype": args.q_dtype,
+                       "agent_steps_per_step": world * steps_per_episode,
+                       "parallelism": f"scenario-sharded x{world} (replicas, no data-path collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
+                         "kernel": "episode_kernel<2,double>", "kernel_ms": kernel_ms,
+                         "algorithmic_bytes_per_agent_step": bpa,
+                         "algorithmic_bytes_per_launch": bpa * steps_per_episode,
+                         "timed_launches": int(len(kms))},
+            "mean_episode_reward": ep_reward,
+        }
+        if traffic:
+            out["roofline"]["traffic_source"] = traffic.get("source")
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, N=N, R=R, T=T)
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -125,6 +125,7 @@ typedef struct p2pmg_episode_args {
 
 /* version / defaults */
 int p2pmg_abi_version(void);
+int p2pmg_device_count(int* count); /* visible HIP devices (0 on a host without GPUs) */
 int p2pmg_config_default(p2pmg_config* cfg); /* the reference constants, S = 1, N = 2, R = 1, T = 96 */
 
 /* lifetime */
@@ -155,6 +156,10 @@ int p2pmg_run_episode(p2pmg_ctx* ctx, const p2pmg_episode_args* args);
 int p2pmg_get_record(p2pmg_ctx* ctx, int which, void* host);   /* one P2PMG_REC_* bit */
 int p2pmg_get_episode_reward(p2pmg_ctx* ctx, float* host);     /* [S]: sum_t mean_i r (community.py:179) */
 int p2pmg_last_kernel_ms(p2pmg_ctx* ctx, float* ms);           /* HIP-event time of the last episode kernel */
+/* HIP-event durations (ms) of the episode kernels launched since the last reset, oldest first
+ * (ring of the last 4096 launches, on the context's stream); *count = entries written. */
+int p2pmg_kernel_times(p2pmg_ctx* ctx, float* ms, int max, int* count);
+int p2pmg_reset_kernel_times(p2pmg_ctx* ctx);
 
 /* batched primitives (device) for unit parity against the reference functions */
 int p2pmg_rc_step(p2pmg_ctx* ctx, int n, const float* t_out, const float* t_in, const float* t_m,

@@ -27,7 +27,8 @@ EXPORTS = [
     "p2pmg_set_temperatures", "p2pmg_get_temperatures", "p2pmg_reset_temperatures_philox",
     "p2pmg_set_replay_codes", "p2pmg_zero_q", "p2pmg_set_q", "p2pmg_get_q", "p2pmg_run_episode",
     "p2pmg_get_record", "p2pmg_get_episode_reward", "p2pmg_last_kernel_ms", "p2pmg_rc_step",
-    "p2pmg_state_indices", "p2pmg_replay_decode",
+    "p2pmg_state_indices", "p2pmg_replay_decode", "p2pmg_device_count", "p2pmg_kernel_times",
+    "p2pmg_reset_kernel_times",
 ]
 
 
@@ -91,6 +92,9 @@ def _declare(lib):
         "p2pmg_rc_step": ([vp, i32, fp, fp, fp, fp, fp, fp], i32),
         "p2pmg_state_indices": ([vp, i32, fp, vp], i32),
         "p2pmg_replay_decode": ([vp, sz, sz, vp, sz, vp, C.POINTER(sz)], i32),
+        "p2pmg_device_count": ([C.POINTER(C.c_int)], i32),
+        "p2pmg_kernel_times": ([vp, fp, i32, C.POINTER(C.c_int)], i32),
+        "p2pmg_reset_kernel_times": ([vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -137,10 +141,15 @@ def default_config() -> Config:
     return cfg
 
 
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().p2pmg_device_count(C.byref(n)), what="device_count")
+    return int(n.value)
+
+
 def gpu_available() -> bool:
-    """True if a HIP device is visible (torch is only consulted for device counting)."""
+    """True if a HIP device is visible (asked through libp2pmg itself, not torch)."""
     try:
-        import torch
-        return torch.cuda.is_available() and torch.cuda.device_count() > 0
+        return device_count() > 0
     except Exception:  # noqa: BLE001
         return False

@@ -27,6 +27,9 @@ struct p2pmg_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  static constexpr int kRing = 4096;
+  std::vector<hipEvent_t> ring;  // 2 * kRing events: start/stop of each episode kernel
+  long long n_timed = 0;          // launches recorded since the last reset
   // device buffers
   float* env = nullptr;
   int n_env = 0;
@@ -98,6 +101,14 @@ int ensure_records(p2pmg_ctx* c, int mask) {
 extern "C" {
 
 int p2pmg_abi_version(void) { return P2PMG_ABI_VERSION; }
+
+int p2pmg_device_count(int* count) {
+  if (!count) return P2PMG_E_INVALID;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return P2PMG_OK;
+}
 
 int p2pmg_config_default(p2pmg_config* cfg) {
   if (!cfg) return P2PMG_E_INVALID;
@@ -201,6 +212,8 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   for (auto& b : c->rec_f32) dfree(b);
   dfree(c->rec_action);
   dfree(c->rec_index);
+  for (auto& ev : c->ring)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -453,11 +466,20 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
       p.rng = 0;
     }
   }
+  if (c->ring.empty()) {
+    c->ring.assign(2 * p2pmg_ctx::kRing, nullptr);
+    for (auto& ev : c->ring) HIP_TRY(c, hipEventCreate(&ev));
+  }
+  const int slot = (int)(c->n_timed % p2pmg_ctx::kRing);
+  hipEvent_t r0 = c->ring[2 * slot], r1 = c->ring[2 * slot + 1];
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
+  HIP_TRY(c, hipEventRecord(r0, c->stream));
   hipError_t e = p2pmg::launch_episode(p, g.q_dtype, c->stream);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));
+  HIP_TRY(c, hipEventRecord(r1, c->stream));
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
+  c->n_timed++;
   return P2PMG_OK;
 }
 
@@ -466,6 +488,27 @@ int p2pmg_last_kernel_ms(p2pmg_ctx* c, float* ms) {
   if (!c->timed) return fail(c, P2PMG_E_STATE, "no episode launched yet");
   HIP_TRY(c, hipEventSynchronize(c->ev1));
   HIP_TRY(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return P2PMG_OK;
+}
+
+int p2pmg_kernel_times(p2pmg_ctx* c, float* ms, int max, int* count) {
+  if (!c || !ms || max < 0 || !count) return P2PMG_E_INVALID;
+  const long long n = c->n_timed < p2pmg_ctx::kRing ? c->n_timed : p2pmg_ctx::kRing;
+  const long long first = c->n_timed - n;
+  int w = 0;
+  for (long long k = first; k < c->n_timed && w < max; ++k, ++w) {
+    const int slot = (int)(k % p2pmg_ctx::kRing);
+    HIP_TRY(c, hipEventSynchronize(c->ring[2 * slot + 1]));
+    HIP_TRY(c, hipEventElapsedTime(&ms[w], c->ring[2 * slot], c->ring[2 * slot + 1]));
+  }
+  *count = w;
+  return P2PMG_OK;
+}
+
+int p2pmg_reset_kernel_times(p2pmg_ctx* c) {
+  if (!c) return P2PMG_E_INVALID;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->n_timed = 0;
   return P2PMG_OK;
 }
 

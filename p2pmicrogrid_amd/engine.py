@@ -171,6 +171,16 @@ class DeviceCommunityBatch:
         self._chk(self.L.p2pmg_last_kernel_ms(self._ctx, C.byref(ms)), "last_kernel_ms")
         return float(ms.value)
 
+    def kernel_times(self, max_n: int = 4096) -> np.ndarray:
+        """HIP-event durations (ms) of the episode kernels since the last reset (syncs)."""
+        out = np.empty(max_n, F32)
+        n = C.c_int(0)
+        self._chk(self.L.p2pmg_kernel_times(self._ctx, out, max_n, C.byref(n)), "kernel_times")
+        return out[:n.value].copy()
+
+    def reset_kernel_times(self):
+        self._chk(self.L.p2pmg_reset_kernel_times(self._ctx), "reset_kernel_times")
+
     def get_record(self, name: str) -> np.ndarray:
         """[T, S, N] for per-step records, [T, R+1, S, N] for action/index."""
         bit = _lib.REC[name]

@@ -1,0 +1,115 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every symbol declared in
+include/p2pmg.h (no compute calls needing a GPU), the native replay decoder reproduces the
+reference's np.random consumption, datasets follow the reference schema, bench helpers."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle.restatement import reference_replay_codes
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "p2pmg.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(p2pmg_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from p2pmicrogrid_amd import _lib
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_lib.EXPORTS)
+    assert L.p2pmg_abi_version() == 1
+
+
+def test_config_default_matches_reference_constants():
+    from p2pmicrogrid_amd import _lib
+    c = _lib.default_config()
+    f = np.float32
+    assert (c.n_agents, c.rounds, c.horizon, c.n_actions) == (2, 1, 96, 3)
+    assert c.alpha == 1e-5 and c.gamma == 0.9
+    assert list(c.hp_levels)[:3] == [0.0, 1500.0, 3000.0]
+    assert f(c.inv_ri) == f(1 / 8.64e-4) and f(c.inv_ci) == f(1 / (2.44e6 * 2))
+    assert f(c.inv_rvent) == f(1 / 7.98e-3) and f(c.inv_re) == f(1 / 1.05e-2) and f(c.inv_cm) == f(1 / 9.4e7)
+    assert f(c.one_minus_frad) == f(1 - 0.3) and f(c.kilo) == f(1e-3)
+    # SURVEY.md §3.4 bit patterns
+    bits = lambda x: int(np.float32(x).view(np.uint32))  # noqa: E731
+    assert bits(c.inv_ri) == 0x4490ad09 and bits(c.inv_rvent) == 0x42faa067 and bits(c.inv_re) == 0x42be79e8
+    assert bits(c.inv_ci) == 0x345c0771 and bits(c.inv_cm) == 0x3236c3bb
+
+
+@pytest.mark.parametrize("eps", [0.0, 0.2, 0.81, 1.0])
+def test_native_replay_decoder_matches_reference_stream(eps):
+    from p2pmicrogrid_amd.rng import ReferenceRNG
+    a, b = np.random.RandomState(42), np.random.RandomState(42)
+    for T, R, N in ((96, 1, 2), (17, 3, 5)):
+        c1 = ReferenceRNG(a).episode_codes(T, R, N, eps)
+        c2 = reference_replay_codes(b, T, R, N, eps)
+        assert np.array_equal(c1, c2)
+        # the stream continues identically (reset normals come next in the reference)
+        assert a.normal(21, 0.3) == b.normal(21, 0.3)
+
+
+def test_reference_rng_community_order():
+    from p2pmicrogrid_amd.rng import ReferenceRNG
+    rs = np.random.RandomState(42)
+    rng = ReferenceRNG(np.random.RandomState(42))
+    lr, pr = rng.community_ratings(2, False)
+    assert np.array_equal(lr, rs.normal(0.7, 0.2, 2)) and np.array_equal(pr, rs.normal(4, 0.2, 2))
+    t_in, t_m = rng.initial_temperature(21.0, False)
+    want_m = np.float32(rs.normal(21.0, 0.3, 1)[0])
+    want_in = np.float32(rs.normal(21.0, 0.3, 1)[0])
+    assert t_m == want_m and t_in == want_in  # T_m is drawn first at __init__ (heating.py:101-104)
+    t_in, t_m = rng.reset_temperature(21.0, False)
+    want_in = np.float32(rs.normal(21.0, 0.3, 1)[0])
+    want_m = np.float32(rs.normal(21.0, 0.3, 1)[0])
+    assert t_in == want_in and t_m == want_m  # T_in first at reset (heating.py:149-152)
+
+
+def test_dataset_schema_and_roll():
+    from p2pmicrogrid_amd import dataset as ds
+    env_df, agent_dfs = ds.get_train_data()
+    assert list(env_df.columns) == ["time", "temperature"] and len(env_df) == 7 * 96
+    assert len(agent_dfs) == 5 and all(list(a.columns) == ["load", "pv"] for a in agent_dfs)
+    assert env_df["time"].min() == 0.0 and env_df["time"].max() == 95 / 96
+    assert all(abs(a["load"].max() - 1.0) < 1e-12 and abs(a["pv"].max() - 1.0) < 1e-12 for a in agent_dfs)
+    d = ds.dataframe_to_dataset(env_df)
+    assert d.data.dtype == np.float32 and np.array_equal(d.rolled, np.roll(d.data, -1, axis=0))
+    assert len(d) == 672
+    pairs = list(d)
+    assert np.array_equal(pairs[-1][1], d.data[0])
+
+
+def test_scenario_batch_is_shard_independent():
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    full = scenario_batch(600, 2, 96)
+    part = scenario_batch(250, 2, 96, first_scenario=300)
+    for k in ("load_w", "pv_w", "max_in", "t_in0", "t_m0", "t_out"):
+        assert np.array_equal(getattr(part, k), getattr(full, k)[300:550]), k
+    assert np.all(full.max_in == np.float32(np.maximum(full.load_ratings, full.pv_ratings) * 1.1 * 1e3))
+
+
+def test_price_table_matches_oracle():
+    from oracle.restatement import prices
+    from p2pmicrogrid_amd.engine import price_table
+    t = (np.arange(96) / 96).astype(np.float32)
+    for a, b in zip(price_table(t), prices(t)):
+        assert np.array_equal(a, b)
+
+
+def test_bench_helpers():
+    import bench
+    assert bench.epsilon_at(0) == 0.81 and bench.epsilon_at(1) == bench.epsilon_at(50) == 0.81 * 0.9
+    assert bench.epsilon_at(51) == 0.81 * 0.9 * 0.9 and bench.epsilon_at(100000) == 0.1
+    assert bench.algorithmic_bytes_per_agent_step(1, 4) == 60  # SURVEY §8(d) 76 B minus the 16 B of state
+    assert bench.algorithmic_bytes_per_agent_step(1, 8) == 104
+
+
+def test_device_count_without_gpu_is_zero_or_more():
+    from p2pmicrogrid_amd import _lib
+    assert _lib.device_count() >= 0
