@@ -166,6 +166,15 @@ int p2pmg_rc_step(p2pmg_ctx* ctx, int n, const float* t_out, const float* t_in, 
                   const float* hp, float* t_in_new, float* t_m_new);
 int p2pmg_state_indices(p2pmg_ctx* ctx, int n, const float* obs /* [n][4] */, int32_t* idx /* [n][4] */);
 
+/* Standalone QActor calls (rl.py:89-129) on the context's per-agent tables, applied IN ORDER
+ * by one device thread: for entry k, s = indices(s_obs[k]); a = codes[k] == P2PMG_GREEDY ?
+ * argmax Q[agent[k], s] (first max) : codes[k]; q_out[k] = greedy ? Q[s, a] : 0 (select_action /
+ * greedy_action); if train, Q[s, a] += alpha * ((reward[k] + gamma * max Q[ns]) - Q[s, a])
+ * (QActor.train).  ns_obs/rewards may be NULL when train == 0. */
+int p2pmg_q_calls(p2pmg_ctx* ctx, int n, const int32_t* agents, const float* s_obs /* [n][4] */,
+                  const uint8_t* codes, const float* rewards, const float* ns_obs /* [n][4] */,
+                  int train, int32_t* actions_out, double* q_out);
+
 /* host-only: decode a block of legacy-MT19937 32-bit words into replay codes, consuming words
  * exactly as rand() (2 words) and choice(3) (masked rejection, 1 word per try) do.
  * eps for decision k is eps[k % n_eps].  Returns P2PMG_E_INVALID if the words run out. */

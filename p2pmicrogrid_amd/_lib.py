@@ -28,7 +28,7 @@ EXPORTS = [
     "p2pmg_set_replay_codes", "p2pmg_zero_q", "p2pmg_set_q", "p2pmg_get_q", "p2pmg_run_episode",
     "p2pmg_get_record", "p2pmg_get_episode_reward", "p2pmg_last_kernel_ms", "p2pmg_rc_step",
     "p2pmg_state_indices", "p2pmg_replay_decode", "p2pmg_device_count", "p2pmg_kernel_times",
-    "p2pmg_reset_kernel_times",
+    "p2pmg_reset_kernel_times", "p2pmg_q_calls",
 ]
 
 
@@ -95,6 +95,7 @@ def _declare(lib):
         "p2pmg_device_count": ([C.POINTER(C.c_int)], i32),
         "p2pmg_kernel_times": ([vp, fp, i32, C.POINTER(C.c_int)], i32),
         "p2pmg_reset_kernel_times": ([vp], i32),
+        "p2pmg_q_calls": ([vp, i32, vp, vp, vp, vp, vp, i32, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

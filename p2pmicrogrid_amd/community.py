@@ -1,0 +1,242 @@
+"""Community orchestration (mirrors microgrid/community.py:33-423).
+
+``CommunityMicrogrid(timeline, agents, rounds)`` keeps the reference's interface; each
+``train_episode`` / ``run`` is ONE device launch (p2pmg_run_episode) over the whole episode:
+negotiation rounds, market clearing, costs, rewards, TD updates and the RC update of every
+agent.  Exploration is replayed from the global ``np.random`` in the reference's consumption
+order, so a seeded reference script and this package draw identical
+streams.  Database logging, plotting and the REST data client are out of scope.
+"""
+from __future__ import annotations
+
+import collections
+import os
+import statistics
+import time
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import dataset as ds
+from . import setup
+from .agent import ActingAgent, Agent, GridAgent, QAgent
+from .engine import DeviceCommunityBatch, price_table
+from .environment import env
+from .heating import HeatPump, HPHeating
+from .production import PV, Prosumer
+from .rng import ReferenceRNG
+from .storage import NoStorage
+
+F32 = np.float32
+
+
+class CommunityMicrogrid:
+
+    def __init__(self, timeline, agents: List[ActingAgent], rounds: int, q_dtype: Optional[str] = None,
+                 device: Optional[int] = None) -> None:
+        self.timeline = timeline
+        self.time_length = len(timeline)
+        self.agents = agents
+        self.grid = GridAgent()
+        self._rounds = rounds
+        self.decisions = np.zeros((len(env), self._rounds + 1, len(self.agents)))
+        self._q_dtype = q_dtype or setup.q_dtype
+        self._device = setup.device if device is None else device
+        self._engine: Optional[DeviceCommunityBatch] = None
+        self._uploaded: Dict[str, Any] = {}
+        self._rng = ReferenceRNG()
+
+    # ------------------------------------------------------------ device state
+    def _ensure_engine(self) -> DeviceCommunityBatch:
+        T, N = len(env), len(self.agents)
+        if self._engine is None or self._engine.T != T:
+            if self._engine is not None:  # horizon changed: carry the learned tables over
+                tables = self._engine.get_q()
+            else:
+                tables = None
+            self._engine = DeviceCommunityBatch(1, N, self._rounds, T, q_dtype=self._q_dtype, device=self._device)
+            for i, a in enumerate(self.agents):
+                if tables is None:
+                    a.actor.bind(self._engine, i)
+                else:
+                    a.actor._engine = None
+                    a.actor.set_qtable(tables[i])
+                    a.actor.bind(self._engine, i)
+            self._uploaded = {}
+        eng = self._engine
+        if self._uploaded.get("env") != env.version:
+            time_f, t_out = env.arrays()
+            eng.set_env(time_f, t_out, *price_table(time_f))
+            self._uploaded["env"] = env.version
+        prof_key = tuple((id(a._load), id(a.pv), id(getattr(a.pv, "pv", None) and a.pv.pv.production))
+                         for a in self.agents)
+        if self._uploaded.get("prof") != prof_key:
+            load = np.stack([a.load_series(T) for a in self.agents])[None]
+            pv = np.stack([a.pv.series(T) for a in self.agents])[None]
+            eng.set_profiles(load, pv)
+            eng.set_max_in(np.array([F32(a.max_in) for a in self.agents], F32)[None])
+            self._uploaded["prof"] = prof_key
+        return eng
+
+    def _push_temperatures(self, eng):
+        t_in = np.array([a.heating.temperature[0] for a in self.agents], F32)
+        t_m = np.array([a.heating.building_mass_temperature[0] for a in self.agents], F32)
+        eng.set_temperatures(t_in[None], t_m[None])
+
+    def _pull_records(self, eng, T):
+        act = eng.get_record("action")[:, :, 0, :]  # [T, R+1, N]
+        levels = np.array([a.heating.hp.max_power for a in self.agents])
+        self.decisions = np.array([0.0, 0.5, 1.0])[act] * levels[None, None, :]
+        return act
+
+    # ------------------------------------------------------------ the reference API
+    def train_episode(self, all_rewards=None, all_losses=None, _rewards=None, _losses=None) -> Tuple[float, float]:
+        """community.py:149-182: one training episode; returns (sum_t mean_i reward, 0 loss)."""
+        eng = self._ensure_engine()
+        T, N = eng.T, eng.N
+        self._push_temperatures(eng)
+        eps = [a.actor._epsilon for a in self.agents]
+        codes = self._rng.episode_codes(T, self._rounds, N, eps)
+        eng.set_replay_codes(codes)
+        eng.run_episode("train", "replay", epsilon=float(eps[0]), record=("reward", "action"))
+        self._pull_records(eng, T)
+        self.last_rewards = eng.get_record("reward")[:, 0, :]
+        avg_reward = float(eng.episode_reward()[0])
+        for agent in self.agents:  # reset iterators + new T0 (community.py:172-174)
+            agent.reset()
+        return avg_reward, 0.0
+
+    def run(self) -> Tuple[np.ndarray, np.ndarray]:
+        """community.py:95-123: greedy rollout; returns (grid + p2p power [T, N], costs [T, N])."""
+        eng = self._ensure_engine()
+        T = eng.T
+        self._push_temperatures(eng)
+        rec = ("grid", "p2p", "cost", "t_in", "action")
+        eng.run_episode("greedy", record=rec)
+        r = eng.get_records(rec)
+        self._pull_records(eng, T)
+        t_in, t_m = eng.get_temperatures()
+        hist = r["t_in"][:, 0, :]
+        for i, a in enumerate(self.agents):
+            a.heating._history = [float(x) for x in hist[:, i]]
+            a.heating._power_history = list(self.decisions[:, -1, i])
+            a.heating.set_state(t_in[0, i], t_m[0, i])
+        power = (r["grid"][:, 0, :] + r["p2p"][:, 0, :]).astype(F32)
+        return power, r["cost"][:, 0, :]
+
+    def init_buffers(self) -> None:
+        """community.py:125-147 fills DQN replay buffers; tabular agents have none."""
+        if any(isinstance(a, QAgent) for a in self.agents):
+            return
+        raise NotImplementedError("DQN agents are not available in this build yet")
+
+    def _step(self) -> None:
+        for agent in self.agents:
+            agent.step()
+        self.grid.step()
+
+    def reset(self) -> None:
+        for agent in self.agents:
+            agent.reset()
+        self.grid.reset()
+        self.decisions = np.zeros((len(env), self._rounds + 1, len(self.agents)))
+
+
+def get_community(agent_constructor: Callable[..., ActingAgent], n_agents: int,
+                  homogeneous: bool = False, rounds_: Optional[int] = None) -> CommunityMicrogrid:
+    """community.py:198-234 with the same np.random consumption (ratings, then per agent
+    HPHeating T_m, T_in) and the same derived quantities."""
+    env_df, agent_dfs = ds.get_train_data()
+    if homogeneous:
+        agent_dfs = [agent_dfs[0]] * n_agents
+    timeline = env_df['time'].map(lambda t: int(t * setup.MINUTES_PER_HOUR / setup.TIME_SLOT * setup.HOURS_PER_DAY))
+    agents: List[ActingAgent] = []
+    rng = ReferenceRNG()
+    load_ratings, pv_ratings = rng.community_ratings(n_agents, homogeneous)
+    Agent.reset_ids()
+    for i in range(n_agents):
+        max_power = max(load_ratings[i], pv_ratings[i])
+        safety = 1.1
+        agent_load = ds.dataframe_to_dataset(agent_dfs[i % len(agent_dfs)]['load'] * load_ratings[i] * 1e3)
+        agent_pv = ds.dataframe_to_dataset(agent_dfs[i % len(agent_dfs)]['pv'] * pv_ratings[i] * 1e3)
+        agents.append(agent_constructor(agent_load,
+                                        Prosumer(PV(peak_power=pv_ratings[i] * 1e3, production=agent_pv)),
+                                        NoStorage(),
+                                        HPHeating(HeatPump(cop=3.0, max_power=3 * 1e3, power=0.0), 21.0, rng=rng),
+                                        max_in=max_power * safety * 1e3,
+                                        max_out=-(max_power + safety * 1e3)))
+    env.setup(ds.dataframe_to_dataset(env_df))
+    return CommunityMicrogrid(timeline, agents, setup.rounds if rounds_ is None else rounds_)
+
+
+def get_rl_based_community(n_agents: int, homogeneous: bool) -> CommunityMicrogrid:
+    if setup.implementation == 'tabular':
+        return get_community(QAgent, n_agents, homogeneous=homogeneous)
+    raise NotImplementedError(f"implementation {setup.implementation!r} is not available in this build")
+
+
+def setting_name(nr_agents=None, rounds=None, homogeneous=None) -> str:
+    """community.py:423"""
+    n = setup.nr_agents if nr_agents is None else nr_agents
+    r = setup.rounds if rounds is None else rounds
+    h = setup.homogeneous if homogeneous is None else homogeneous
+    return f'{n}-multi-agent-com-rounds-{r}-{"homo" if h else "hetero"}'
+
+
+def main(load_agents: bool = False, episodes: Optional[int] = None, save: bool = True,
+         verbose: bool = True) -> Dict[str, Any]:
+    """community.py:248-321 training loop (DB logging and plotting out of scope): epsilon decay
+    after episodes 0, 50, ...; checkpoints every ``save_episodes`` and at the end."""
+    setting = setting_name()
+    community = get_rl_based_community(setup.nr_agents, homogeneous=setup.homogeneous)
+    if load_agents:
+        for agent in community.agents:
+            agent.load_from_file(setting, setup.implementation)
+    rewards_q: collections.deque = collections.deque(maxlen=setup.min_episodes_criterion)
+    history = []
+    t0 = time.time()
+    last = setup.max_episodes if episodes is None else setup.starting_episodes + episodes
+    for episode in range(setup.starting_episodes, last):
+        reward, error = community.train_episode()
+        rewards_q.append(reward)
+        history.append(reward)
+        if episode % setup.min_episodes_criterion == 0:
+            if verbose:
+                print(f'Average reward: {statistics.mean(rewards_q):.3f}. Average error: {0.0:.3f}')
+            for agent in community.agents:
+                agent.actor.decay_exploration()
+        if save and (episode + 1) % setup.save_episodes == 0:
+            for agent in community.agents:
+                agent.save_to_file(setting, setup.implementation)
+    if save:
+        for agent in community.agents:
+            agent.save_to_file(setting, setup.implementation)
+    return {"community": community, "rewards": history, "train_time": time.time() - t0}
+
+
+def load_and_run(is_testing: bool = False) -> Dict[int, Dict[str, np.ndarray]]:
+    """community.py:364-412 without the DB sink: greedy evaluation per test/validation day from
+    the saved tables, a fresh start each day; returns per-day power, cost and decisions."""
+    setting = setting_name()
+    community = get_rl_based_community(setup.nr_agents, homogeneous=setup.homogeneous)
+    for agent in community.agents:
+        agent.load_from_file(setting, setup.implementation)
+    env_df, agent_dfs = ds.get_test_data() if is_testing else ds.get_validation_data()
+    days = np.unique(env_df['day'])
+    day_indices = {day: env_df['day'] == day for day in days}
+    env_df = env_df.drop(axis=1, labels='day')
+    if setup.homogeneous:
+        agent_dfs = [agent_dfs[0]] * setup.nr_agents
+    out = {}
+    for day in days:
+        env.setup(ds.dataframe_to_dataset(env_df[day_indices[day]]))
+        community.reset()
+        for i, agent in enumerate(community.agents):
+            lr = 0.7e3 if setup.homogeneous else np.random.normal(0.7, 0.2, 1) * 1e3
+            agent_load = ds.dataframe_to_dataset(agent_dfs[i].loc[day_indices[day], 'load'] * lr)
+            pr = 4e3 if setup.homogeneous else np.random.normal(4, 0.2, 1) * 1e3
+            agent_pv = ds.dataframe_to_dataset(agent_dfs[i].loc[day_indices[day], 'pv'] * pr)
+            agent.set_profiles(agent_load, agent_pv)
+        power, cost = community.run()
+        out[int(day)] = {"power": power, "cost": cost, "decisions": community.decisions.copy()}
+    return out

@@ -60,6 +60,21 @@ hipError_t launch_q_pack(int count, size_t n_states, int n_actions, const void* 
                          int q_dtype, int src_dtype, hipStream_t stream);
 hipError_t launch_q_unpack(int count, size_t n_states, int n_actions, const void* src_pad, void* dst_ref,
                            int q_dtype, int dst_dtype, hipStream_t stream);
+struct QCallParams {
+  int n, train, q_dtype;
+  const int32_t* agents;
+  const float* s_obs;
+  const uint8_t* codes;
+  const float* rewards;
+  const float* ns_obs;
+  int32_t* actions;
+  double* q_out;
+  void* q;
+  uint32_t n_states;
+  int nt, nT, nb, np;
+  double alpha, gamma;
+};
+hipError_t launch_q_calls(const QCallParams& p, hipStream_t stream);
 hipError_t launch_prof_pack(int A, int T, const float* load_w, const float* pv_w, float2* prof,
                             hipStream_t stream);
 

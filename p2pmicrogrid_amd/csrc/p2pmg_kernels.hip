@@ -614,6 +614,30 @@ __global__ void prof_pack_kernel(int A, int T, const float* load_w, const float*
   prof[k] = make_float2(load_w[(size_t)a * T + t], pv_w[(size_t)a * T + t]);
 }
 
+// Standalone QActor calls, applied in order by a single thread (rl.py:89-129).
+template <typename QT>
+__global__ void q_calls_kernel(const QCallParams p) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  for (int k = 0; k < p.n; ++k) {
+    QT* q = reinterpret_cast<QT*>(p.q) + (size_t)p.agents[k] * p.n_states * kQPad;
+    const float* o = p.s_obs + 4 * k;
+    const uint32_t srow = (uint32_t)(((idx_time(o[0], p.nt) * p.nT + idx_temp(o[1], p.nT)) * p.nb +
+                                      idx_plain(o[2], p.nb)) * p.np + idx_plain(o[3], p.np));
+    const Row4<QT> row = load_row(q + srow * kQPad);
+    const int code = p.codes[k];
+    const int a = code == 255 ? argmax3(row) : code;
+    p.actions[k] = a;
+    p.q_out[k] = code == 255 ? (double)row.v[a] : 0.0;
+    if (p.train) {
+      const float* n = p.ns_obs + 4 * k;
+      const uint32_t nrow = (uint32_t)(((idx_time(n[0], p.nt) * p.nT + idx_temp(n[1], p.nT)) * p.nb +
+                                        idx_plain(n[2], p.nb)) * p.np + idx_plain(n[3], p.np));
+      const QT qmax = max3(load_row(q + nrow * kQPad));
+      q[srow * kQPad + a] = td_update(q[srow * kQPad + a], p.rewards[k], qmax, p.alpha, p.gamma);
+    }
+  }
+}
+
 inline unsigned grid_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
@@ -688,6 +712,15 @@ hipError_t launch_q_unpack(int count, size_t n_states, int n_actions, const void
     hipLaunchKernelGGL((q_unpack_kernel<double, float>), g, b, 0, stream, rows, n_actions, (const float*)src_pad, (double*)dst_ref);
   else
     hipLaunchKernelGGL((q_unpack_kernel<float, float>), g, b, 0, stream, rows, n_actions, (const float*)src_pad, (float*)dst_ref);
+  return hipGetLastError();
+}
+
+hipError_t launch_q_calls(const QCallParams& p, hipStream_t stream) {
+  if (p.n <= 0) return hipSuccess;
+  if (p.q_dtype == 0)
+    hipLaunchKernelGGL(q_calls_kernel<double>, dim3(1), dim3(64), 0, stream, p);
+  else
+    hipLaunchKernelGGL(q_calls_kernel<float>, dim3(1), dim3(64), 0, stream, p);
   return hipGetLastError();
 }
 

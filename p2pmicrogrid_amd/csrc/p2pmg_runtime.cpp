@@ -589,6 +589,41 @@ int p2pmg_state_indices(p2pmg_ctx* c, int n, const float* obs, int32_t* idx) {
   return P2PMG_OK;
 }
 
+int p2pmg_q_calls(p2pmg_ctx* c, int n, const int32_t* agents, const float* s_obs, const uint8_t* codes,
+                  const float* rewards, const float* ns_obs, int train, int32_t* actions_out, double* q_out) {
+  if (!c || n < 0 || !agents || !s_obs || !codes || !actions_out || !q_out) return P2PMG_E_INVALID;
+  if (train && (!rewards || !ns_obs)) return fail(c, P2PMG_E_INVALID, "q_calls: train needs rewards and ns_obs");
+  for (int k = 0; k < n; ++k)
+    if (agents[k] < 0 || agents[k] >= c->A) return fail(c, P2PMG_E_INVALID, "q_calls: agent out of range");
+  if (n == 0) return P2PMG_OK;
+  // one staging block: agents | s_obs | ns_obs | rewards | codes | actions | q_out
+  const size_t nb = (size_t)n;
+  const size_t off_s = 0, off_ns = off_s + 16 * nb, off_r = off_ns + 16 * nb, off_a = off_r + 4 * nb,
+               off_act = off_a + 4 * nb, off_q = ((off_act + 4 * nb + 7) / 8) * 8, off_c = off_q + 8 * nb,
+               total = off_c + nb;
+  char* d = nullptr;
+  HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&d), total));
+  hipError_t e = hipMemcpyAsync(d + off_s, s_obs, 16 * nb, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess && train) e = hipMemcpyAsync(d + off_ns, ns_obs, 16 * nb, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess && train) e = hipMemcpyAsync(d + off_r, rewards, 4 * nb, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + off_a, agents, 4 * nb, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + off_c, codes, nb, hipMemcpyHostToDevice, c->stream);
+  const p2pmg_config& g = c->cfg;
+  p2pmg::QCallParams p{n, train ? 1 : 0, g.q_dtype, reinterpret_cast<const int32_t*>(d + off_a),
+                       reinterpret_cast<const float*>(d + off_s), reinterpret_cast<const uint8_t*>(d + off_c),
+                       reinterpret_cast<const float*>(d + off_r), reinterpret_cast<const float*>(d + off_ns),
+                       reinterpret_cast<int32_t*>(d + off_act), reinterpret_cast<double*>(d + off_q), c->q,
+                       (uint32_t)c->n_states, g.n_time_states, g.n_temp_states, g.n_balance_states, g.n_p2p_states,
+                       g.alpha, g.gamma};
+  if (e == hipSuccess) e = p2pmg::launch_q_calls(p, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(actions_out, d + off_act, 4 * nb, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(q_out, d + off_q, 8 * nb, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("q_calls: ") + hipGetErrorString(e));
+  return P2PMG_OK;
+}
+
 int p2pmg_replay_decode(const uint32_t* words, size_t n_words, size_t n_decisions, const double* eps, size_t n_eps,
                         uint8_t* codes, size_t* consumed) {
   if (!words || !eps || n_eps == 0 || !codes) return P2PMG_E_INVALID;

@@ -221,6 +221,25 @@ class DeviceCommunityBatch:
         return idx.reshape(np.shape(obs))
 
 
+def _q_calls(eng: "DeviceCommunityBatch", agents, s_obs, codes, rewards=None, ns_obs=None, train=False):
+    agents = np.ascontiguousarray(np.asarray(agents, dtype=np.int32).ravel())
+    n = agents.size
+    s_obs = np.ascontiguousarray(np.asarray(s_obs, dtype=F32).reshape(n, 4))
+    codes = np.ascontiguousarray(np.asarray(codes, dtype=np.uint8).ravel())
+    acts = np.empty(n, np.int32)
+    qv = np.empty(n, np.float64)
+    if train:
+        rewards = np.ascontiguousarray(np.asarray(rewards, dtype=F32).ravel())
+        ns_obs = np.ascontiguousarray(np.asarray(ns_obs, dtype=F32).reshape(n, 4))
+    eng._chk(eng.L.p2pmg_q_calls(eng._ctx, n, agents.ctypes.data, s_obs.ctypes.data, codes.ctypes.data,
+                                 rewards.ctypes.data if train else None, ns_obs.ctypes.data if train else None,
+                                 int(bool(train)), acts.ctypes.data, qv.ctypes.data), "q_calls")
+    return acts, qv
+
+
+DeviceCommunityBatch.q_calls = _q_calls
+
+
 def unpack_index(packed: np.ndarray) -> np.ndarray:
     """P2PMG_REC_INDEX packing -> [..., 4] (it, iT, ib, ip)."""
     p = np.asarray(packed, dtype=np.int64)

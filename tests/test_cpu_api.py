@@ -1,0 +1,39 @@
+"""CPU tests of the reference-shaped object API (construction only: no device calls)."""
+import numpy as np
+
+
+def test_get_community_consumes_rng_like_reference():
+    from p2pmicrogrid_amd.agent import QAgent
+    from p2pmicrogrid_amd.community import get_community, setting_name
+    from p2pmicrogrid_amd.environment import env
+    np.random.seed(42)
+    com = get_community(QAgent, 2, homogeneous=False)
+    rs = np.random.RandomState(42)
+    lr, pr = rs.normal(0.7, 0.2, 2), rs.normal(4, 0.2, 2)
+    for i, a in enumerate(com.agents):
+        t_m = np.float32(rs.normal(21.0, 0.3, 1)[0])
+        t_in = np.float32(rs.normal(21.0, 0.3, 1)[0])
+        assert a.heating.temperature[0] == t_in and a.heating.building_mass_temperature[0] == t_m
+        assert a.max_in == max(lr[i], pr[i]) * 1.1 * 1e3 and a.id == i
+        assert a.actor._epsilon == 0.81 and a.actor.q_table.shape == (20, 20, 20, 20, 3)
+    assert len(env) == 672 and com.decisions.shape == (672, 2, 2)
+    assert setting_name() == "2-multi-agent-com-rounds-1-hetero"
+    assert np.random.rand() == rs.rand()  # nothing else was drawn
+
+
+def test_unbound_qactor_table_management(tmp_path, monkeypatch):
+    from p2pmicrogrid_amd import rl
+    monkeypatch.setattr(rl, "MODELS_DIR", str(tmp_path))
+    a = rl.QActor(20, 20, 20, 20, epsilon=0.81, decay=0.9)
+    assert not a.q_table.any()
+    t = np.random.RandomState(0).randn(20, 20, 20, 20, 3)
+    a.set_qtable(t)
+    a.save_to_file("x_0", "tabular")
+    b = rl.QActor(20, 20, 20, 20)
+    b.load_from_file("x_0", "tabular")
+    assert np.array_equal(b.q_table, t)
+    a.decay_exploration()
+    assert a._epsilon == 0.81 * 0.9
+    for _ in range(100):
+        a.decay_exploration()
+    assert a._epsilon == 0.1
