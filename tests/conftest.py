@@ -5,8 +5,11 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-if ROOT not in sys.path:
-    sys.path.insert(0, ROOT)
+TESTS = os.path.join(ROOT, "tests")
+for _p in (ROOT, TESTS):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+os.environ["PYTHONPATH"] = os.pathsep.join([ROOT, TESTS] + [x for x in os.environ.get("PYTHONPATH", "").split(os.pathsep) if x])
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 

@@ -1,0 +1,48 @@
+"""Test-only stand-in with the DeviceCommunityBatch interface, computed by the oracle, so the
+multi-process orchestration (sharding, collectives) can be exercised on CPU with gloo."""
+import numpy as np
+
+from oracle import philox
+from oracle.restatement import OracleBatch
+
+
+class OracleEngine:
+    def __init__(self, sh, S, N, R, T, q_dtype, device, seed):
+        self.S, self.N, self.R, self.T, self.seed = S, N, R, T, seed
+        self.gids = (np.arange(sh.first, sh.first + S)[:, None] * N + np.arange(N)[None, :])
+        self.q_dtype = q_dtype
+        self._env = self._prof = self._mi = None
+        self.ob = None
+        self.last = None
+
+    def set_env(self, time, t_out, *prices):
+        self._env = (np.asarray(time, np.float32)[:1], np.asarray(t_out, np.float32))
+
+    def set_profiles(self, load, pv):
+        self._prof = (np.asarray(load, np.float32), np.asarray(pv, np.float32))
+
+    def set_max_in(self, mi):
+        self._mi = np.asarray(mi, np.float32)
+
+    def _ensure(self):
+        if self.ob is None:
+            self.ob = OracleBatch(S=self.S, N=self.N, R=self.R, load_w=self._prof[0], pv_w=self._prof[1],
+                                  max_in=self._mi, env_time=self._env[0], env_tout=self._env[1],
+                                  q_dtype=self.q_dtype)
+        return self.ob
+
+    def set_temperatures(self, t_in, t_m):
+        ob = self._ensure()
+        ob.t_in = np.asarray(t_in, np.float32).reshape(self.S, self.N).copy()
+        ob.t_m = np.asarray(t_m, np.float32).reshape(self.S, self.N).copy()
+
+    def reset_temperatures_philox(self, episode, sigma=0.3):
+        a, b = philox.t0_draws(self.seed, episode, self.gids.ravel(), sigma=sigma)
+        self.set_temperatures(a, b)
+
+    def run_episode(self, mode="train", rng="philox", episode=0, epsilon=0.81, record=(), philox="auto"):
+        self.last = self._ensure().run_episode(mode, rng="philox", seed=self.seed, episode=episode, eps=epsilon,
+                                               agent_ids=self.gids)
+
+    def episode_reward(self):
+        return self.last["episode_reward"]

@@ -1,0 +1,60 @@
+"""world_size-2 gloo runs of the sharded trainer on CPU (oracle-backed stand-in engine):
+sharding + metric collectives reproduce the single-process result scenario for scenario."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from p2pmicrogrid_amd.distributed import ShardedTrainer, shard
+
+S_TOTAL, N, R, T, EPISODES = 9, 2, 1, 24, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oracle_engine import OracleEngine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = ShardedTrainer(S_TOTAL, N, R, T, rank=rank, world=world, engine_factory=OracleEngine)
+    means = [tr.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    per_scen = tr.episode_rewards_global()
+    if rank == 0:
+        q.put((means, per_scen))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_split():
+    parts = [shard(10, r, 4) for r in range(4)]
+    assert [p.count for p in parts] == [3, 3, 2, 2] and [p.first for p in parts] == [0, 3, 6, 8]
+    assert sum(shard(4096, r, 8).count for r in range(8)) == 4096
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_matches_single_process():
+    from oracle_engine import OracleEngine
+    single = ShardedTrainer(S_TOTAL, N, R, T, engine_factory=OracleEngine)
+    means1 = [single.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    per1 = single.episode_rewards_global()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    means2, per2 = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(per1, per2)
+    assert np.allclose(means1, means2, rtol=0, atol=1e-9)
