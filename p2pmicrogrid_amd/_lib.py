@@ -109,8 +109,8 @@ def lib() -> C.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        path = _build.LIB
-        if _build.needs_build():
+        path = os.environ.get("P2PMG_LIB") or _build.LIB
+        if path == _build.LIB and _build.needs_build():
             hipcc = _build.hipcc()
             if os.path.exists(hipcc) or hipcc == "hipcc":
                 try:

@@ -77,6 +77,42 @@ template <typename QT>
 struct Row4 {
   QT v[4];
 };
+
+// x[a] for a in {0,1,2} as two v_cndmask: written in asm because hipcc turns a select chain
+// on a runtime index into a scratch/LDS lookup table (a memory round trip + vmcnt(0) drain)
+__device__ __forceinline__ float sel3(int a, float x0, float x1, float x2) {
+  float r;
+  asm volatile(
+      "v_cmp_eq_u32 vcc, 1, %1\n\t"
+      "v_cndmask_b32 %0, %2, %3, vcc\n\t"
+      "v_cmp_eq_u32 vcc, 2, %1\n\t"
+      "v_cndmask_b32 %0, %0, %4, vcc"
+      : "=&v"(r)
+      : "v"(a), "v"(x0), "v"(x1), "v"(x2)
+      : "vcc");
+  return r;
+}
+__device__ __forceinline__ double sel3(int a, double x0, double x1, double x2) {
+  const uint64_t b0 = (uint64_t)__double_as_longlong(x0), b1 = (uint64_t)__double_as_longlong(x1),
+                 b2 = (uint64_t)__double_as_longlong(x2);
+  const uint32_t lo = __float_as_uint(sel3(a, __uint_as_float((uint32_t)b0), __uint_as_float((uint32_t)b1),
+                                           __uint_as_float((uint32_t)b2)));
+  const uint32_t hi = __float_as_uint(sel3(a, __uint_as_float((uint32_t)(b0 >> 32)),
+                                           __uint_as_float((uint32_t)(b1 >> 32)),
+                                           __uint_as_float((uint32_t)(b2 >> 32))));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// Timing-only ablation builds (scripts/latency_ablation.py): -DP2PMG_ABLATE=1 replaces the
+// episode kernel's Q-row gathers by values derived from the address (no memory access),
+// -DP2PMG_ABLATE=2 replaces f32 divisions by reciprocal multiplies.  Never shipped.
+#ifndef P2PMG_ABLATE
+#define P2PMG_ABLATE 0
+#endif
+#if P2PMG_ABLATE == 2
+#define FDIV(a, b) ((a) * __frcp_rn(b))
+#else
+#define FDIV(a, b) ((a) / (b))
+#endif
 __device__ __forceinline__ Row4<double> load_row(const double* p) {
   const double2 a = *reinterpret_cast<const double2*>(p);
   const double2 b = *reinterpret_cast<const double2*>(p + 2);
@@ -210,6 +246,44 @@ __device__ __forceinline__ EnvRow load_env(const float* e) {
   return EnvRow{v.x, v.y, v.z, v.w, e[4]};
 }
 
+// Loop constants pinned in VGPRs.  The kernel-argument struct has ~60 fields: left in SGPRs
+// they overflow the scalar file and hipcc reloads them from VGPR lanes (v_readlane) on the
+// step's dependency chain.  An opaque v_mov at entry makes each one a VGPR for the whole
+// episode (one wave per SIMD leaves ample VGPRs).
+__device__ __forceinline__ float vpin(float x) {
+  float r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ int vpin(int x) {
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ double vpin(double x) {
+  const uint64_t b = (uint64_t)__double_as_longlong(x);
+  const uint32_t lo = (uint32_t)vpin((int)(uint32_t)b), hi = (uint32_t)vpin((int)(uint32_t)(b >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+struct KC {
+  float setpoint, margin, lower, upper;
+  float inv_ci, inv_cm, inv_ri, inv_re, inv_rvent, c_in, c_m, solar, cop, spm, slot;
+  float mph, kilo, penw, l0, l1, l2;
+  double alpha, gamma;
+  int nt, nT, nb, np;
+};
+__device__ __forceinline__ KC pin_constants(const EpisodeParams& p) {
+  KC k;
+  k.setpoint = vpin(p.setpoint); k.margin = vpin(p.margin); k.lower = vpin(p.lower); k.upper = vpin(p.upper);
+  k.inv_ci = vpin(p.inv_ci); k.inv_cm = vpin(p.inv_cm); k.inv_ri = vpin(p.inv_ri); k.inv_re = vpin(p.inv_re);
+  k.inv_rvent = vpin(p.inv_rvent); k.c_in = vpin(p.c_in); k.c_m = vpin(p.c_m); k.solar = vpin(p.solar);
+  k.cop = vpin(p.cop); k.spm = vpin(p.spm); k.slot = vpin(p.slot); k.mph = vpin(p.mph); k.kilo = vpin(p.kilo);
+  k.penw = vpin(p.penw); k.l0 = vpin(p.hp_levels[0]); k.l1 = vpin(p.hp_levels[1]); k.l2 = vpin(p.hp_levels[2]);
+  k.alpha = vpin(p.alpha); k.gamma = vpin(p.gamma);
+  k.nt = vpin(p.nt); k.nT = vpin(p.nT); k.nb = vpin(p.nb); k.np = vpin(p.np);
+  return k;
+}
+
 // Everything about step t that is known before its negotiation starts.
 struct StepIdx {
   float bal;        // (load - pv) / max_in of this step    agent.py:172-176
@@ -218,13 +292,13 @@ struct StepIdx {
   uint32_t strip;   // row of (it, iT, ib, 0) in the agent's table
   uint32_t nrow;    // next-state row (time_{t+1}, same T_in, bal_{t+1}, p2p = 0)  agent.py:293-296
 };
-__device__ __forceinline__ StepIdx make_step(const EpisodeParams& p, float time_t, float time_n, float bal, float2 f_n,
-                                             float tin, float mi, int ip_zero) {
+__device__ __forceinline__ StepIdx make_step(const KC& p, bool margin_one, float time_t, float time_n, float bal,
+                                             float2 f_n, float tin, float mi, int ip_zero) {
   StepIdx st;
   st.bal = bal;
-  st.baln = (f_n.x - f_n.y) / mi;
+  st.baln = FDIV(f_n.x - f_n.y, mi);
   const float dt = tin - p.setpoint;  // heating.py:118-120 (x / 1.0 == x exactly)
-  const float tnorm = p.margin == 1.0f ? dt : dt / p.margin;
+  const float tnorm = margin_one ? dt : dt / p.margin;
   st.it = idx_time(time_t, p.nt);
   st.iT = idx_temp(tnorm, p.nT);
   st.ib = idx_plain(bal, p.nb);
@@ -251,16 +325,15 @@ struct CodeWords {
   uint32_t w0, w1;  // loaded words
   uint64_t gen;     // in-kernel Philox word (p.rng == 1)
 };
-__device__ __forceinline__ CodeWords step_codes(const EpisodeParams& p, int t, int a) {
-  const int R1 = p.R + 1;
-  const int W = (R1 + 3) >> 2;  // code words [T][W][A] (replay upload or Philox pre-pass)
-  const size_t k0 = ((size_t)t * W) * p.A + a;
+__device__ __forceinline__ CodeWords step_codes(const EpisodeParams& p, const uint32_t* codes_a, size_t off, int t,
+                                                int a, int W) {
+  // code words [T][W][A] (replay upload or Philox pre-pass); off = t * W * A
   CodeWords c;
-  c.w0 = p.codes[k0];
-  c.w1 = p.codes[W > 1 ? k0 + p.A : k0];
+  c.w0 = codes_a[off];
+  c.w1 = codes_a[W > 1 ? off + (size_t)p.A : off];
   c.gen = ~0ull;
   if (p.rng == 1) {
-    for (int r = 0; r < R1; ++r) {
+    for (int r = 0; r <= p.R; ++r) {
       const uint64_t v = philox_code(p, t, r, p.agent_offset + (uint32_t)a);
       c.gen = (c.gen & ~(0xFFull << (8 * r))) | (v << (8 * r));
     }
@@ -294,10 +367,7 @@ __device__ __forceinline__ Row4<QT> patched(Row4<QT> r, uint32_t addr, const Pat
 
 // heat-pump power of an action without a dynamically indexed kernarg array (that compiles to
 // a global load + vmcnt(0) on the critical path)
-__device__ __forceinline__ float hp_of(const EpisodeParams& p, int act) {
-  const float l0 = p.hp_levels[0], l1 = p.hp_levels[1], l2 = p.hp_levels[2];
-  return act == 0 ? l0 : (act == 1 ? l1 : l2);
-}
+__device__ __forceinline__ float hp_of(const KC& k, int act) { return sel3(act, k.l0, k.l1, k.l2); }
 
 // ----------------------------------------------------------------- the episode kernel
 // One launch = one episode of T timesteps for every scenario (train_episode / run).
@@ -307,6 +377,15 @@ __device__ __forceinline__ float hp_of(const EpisodeParams& p, int act) {
 //     the next-state row, is known as soon as the previous step's final action is: both are
 //     issued right after that action, before the previous step's market/reward/TD work;
 //   * a TD store that hits one of those prefetched rows patches the register copy.
+template <typename QT>
+__device__ __forceinline__ Row4<QT> gather_row(const QT* p) {
+#if P2PMG_ABLATE == 1 || P2PMG_ABLATE == 4
+  const uint32_t x = (uint32_t)(reinterpret_cast<uintptr_t>(p) >> 5);
+  return Row4<QT>{{(QT)(x & 3), (QT)((x >> 2) & 3), (QT)((x >> 4) & 3), (QT)0}};
+#else
+  return load_row(p);
+#endif
+}
 template <int N, typename QT>
 __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   constexpr int G = pow2ceil(N);
@@ -324,16 +403,20 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   const int s_env = p.n_env == 1 ? 0 : (s < p.S ? s : 0);
   const int T = p.T;
   const int R1 = p.R + 1;
+  const int W = (R1 + 3) >> 2;
   const bool train = p.mode == 0;
+  const bool margin_one = p.margin == 1.0f;
+  const uint32_t rec = (uint32_t)p.record;
   const size_t A = (size_t)p.A;
+  const KC k = pin_constants(p);  // loop constants in VGPRs (no SGPR spill reloads on the chain)
 
   const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
   QT* __restrict__ q = reinterpret_cast<QT*>(p.q) + (size_t)a * n_states * kQPad;
   const float mi = active ? p.max_in[a] : 1.0f;
-  float tin = active ? p.t_in[a] : p.setpoint;
-  float tm = active ? p.t_m[a] : p.setpoint;
+  float tin = active ? p.t_in[a] : k.setpoint;
+  float tm = active ? p.t_m[a] : k.setpoint;
   // round 0 and the next state both have p2p = mean(-0 ... -0) / max_in = 0 (agent.py:203, community.py:161)
-  const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, p.np);
+  const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, k.np);
 
   // running offsets (no 64-bit multiplies in the loop)
   const float* envb = p.env + (size_t)s_env * kEnvStride;
@@ -342,16 +425,26 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   const float2* profb = p.prof + a;
   const size_t prof_end = A * T;
   auto prof_at = [&](size_t off) { return profb[off]; };  // inactive lanes read agent 0 (a = 0)
+  const uint32_t* codes_a = p.codes + a;
+  const size_t code_step = (size_t)W * A;
+  float* rec_reward = p.rec_reward + a;
+  float* rec_cost = p.rec_cost + a;
+  float* rec_grid = p.rec_grid + a;
+  float* rec_p2p = p.rec_p2p + a;
+  float* rec_tin = p.rec_tin + a;
+  uint8_t* rec_action = p.rec_action + a;
+  int32_t* rec_index = p.rec_index + a;
   auto adv = [](size_t off, size_t step, size_t end) { off += step; return off >= end ? off - end : off; };
   size_t e1o = adv(0, env_step, env_end), e2o = adv(e1o, env_step, env_end);
   size_t f1o = adv(0, A, prof_end), f2o = adv(f1o, A, prof_end);
+  size_t c1o = (T > 1) ? code_step : 0;  // code words of step t + 1 (wrapping to 0 on the last step)
 
   EnvRow e0 = load_env(envb);
   EnvRow e1 = load_env(envb + e1o);
   const float2 f0 = prof_at(0);
   float2 f1 = prof_at(f1o);
-  StepIdx st = make_step(p, e0.time, e1.time, (f0.x - f0.y) / mi, f1, tin, mi, ip_zero);
-  uint64_t cw = code_word(p, step_codes(p, 0, a), active);
+  StepIdx st = make_step(k, margin_one, e0.time, e1.time, FDIV(f0.x - f0.y, mi), f1, tin, mi, ip_zero);
+  uint64_t cw = code_word(p, step_codes(p, codes_a, 0, 0, a, W), active);
   // Q rows are loaded unconditionally (a load under a divergent branch is waited for at the
   // join, which would serialise the prefetch); a row that is not needed aliases one that is
   // loaded anyway, so it costs no HBM traffic.  Inactive lanes read agent 0's table.
@@ -361,17 +454,22 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   };
   uint32_t a0 = row0_addr(st, cw);
   uint32_t aN = train ? st.nrow : a0;
-  Row4<QT> row0 = load_row(q + a0 * kQPad);
-  Row4<QT> rowN = load_row(q + aN * kQPad);
+  Row4<QT> row0 = gather_row(q + a0 * kQPad);
+  Row4<QT> rowN = gather_row(q + aN * kQPad);
   Patch<QT> pat{0xFFFFFFFFu, 0, (QT)0};
   float ep_sum = 0.0f;
   size_t tA = 0;
 
   for (int t = 0; t < T; ++t, tA += A) {
     // prefetch ahead: env/profile two steps, exploration codes one step
+#if P2PMG_ABLATE >= 3
+    const EnvRow e2 = load_env(envb);
+    const float2 f2 = prof_at(0);
+#else
     const EnvRow e2 = load_env(envb + e2o);
     const float2 f2 = prof_at(f2o);
-    const CodeWords cw1r = step_codes(p, t + 1 == T ? 0 : t + 1, a);
+#endif
+    const CodeWords cw1r = step_codes(p, codes_a, c1o, t + 1 == T ? 0 : t + 1, a, W);
 
     float row[N];
     float col[N];
@@ -391,13 +489,13 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
         float acc = 0.0f;
 #pragma unroll
         for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : col[j]));
-        ip = idx_plain(div_n<N>(acc) / mi, p.np);
+        ip = idx_plain(FDIV(div_n<N>(acc), mi), k.np);
         // the final round's row is needed for the TD update even when exploring
         const bool need = code == 255 || (train && r == R1 - 1);
-        rowR = load_row(q + (need ? st.strip + (uint32_t)ip : a0) * kQPad);
+        rowR = gather_row(q + (need ? st.strip + (uint32_t)ip : a0) * kQPad);
       }
       act = code == 255 ? argmax3(rowR) : code;  // QAgent._act / take_decision (agent.py:271-289)
-      hp = hp_of(p, act);
+      hp = hp_of(k, act);
 
       // RLAgent._divide_power agent.py:186-195 on out = bal * max_in + hp (agent.py:210)
       const float out = (st.bal * mi) + hp;
@@ -417,26 +515,26 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
         for (int j = 0; j < N; ++j) row[j] = ev;
       } else {
 #pragma unroll
-        for (int j = 0; j < N; ++j) row[j] = (out * fabsf(f[j])) / tot;
+        for (int j = 0; j < N; ++j) row[j] = FDIV(out * fabsf(f[j]), tot);
       }
-      if (active) {
-        const size_t k = (tA * R1) + (size_t)r * A + a;
-        if (p.record & 32) p.rec_action[k] = (uint8_t)act;
-        if (p.record & 64) p.rec_index[k] = st.it | (st.iT << 8) | (st.ib << 16) | (ip << 24);
+      if (active && (rec & 96u)) {
+        const size_t kk = (tA * R1) + (size_t)r * A;
+        if (rec & 32u) rec_action[kk] = (uint8_t)act;
+        if (rec & 64u) rec_index[kk] = st.it | (st.iT << 8) | (st.ib << 16) | (ip << 24);
       }
     }
 
     // CommunityMicrogrid._step -> HPHeating.step (community.py:184-188, heating.py:138-143):
     // computed now so the next step's rows can be issued before this step's market work
     float tin1 = tin, tm1 = tm;
-    rc_update(p, e0.t_out, hp, tin1, tm1);
+    rc_update(k, e0.t_out, hp, tin1, tm1);
     // (after the last step this prefetches a wrapped, unused step: harmless valid addresses)
-    const StepIdx st1 = make_step(p, e1.time, e2.time, st.baln, f2, tin1, mi, ip_zero);
+    const StepIdx st1 = make_step(k, margin_one, e1.time, e2.time, st.baln, f2, tin1, mi, ip_zero);
     const uint64_t cw1 = code_word(p, cw1r, active);
     const uint32_t a0n = row0_addr(st1, cw1);
     const uint32_t aNn = train ? st1.nrow : a0n;
-    const Row4<QT> row0n = load_row(q + a0n * kQPad);
-    const Row4<QT> rowNn = load_row(q + aNn * kQPad);
+    const Row4<QT> row0n = gather_row(q + a0n * kQPad);
+    const Row4<QT> rowNn = gather_row(q + aNn * kQPad);
     pat.row = 0xFFFFFFFFu;
 
     // CommunityMicrogrid._assign_powers community.py:45-54 on the final P (diagonal kept)
@@ -453,27 +551,26 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
     // CommunityMicrogrid._compute_costs community.py:56-65
     float cost = (g >= 0.0f) ? g * e0.buy : g * e0.inj;
     cost = cost + pp * e0.p2p;
-    cost = (cost * p.slot) / p.mph;
-    cost = cost * p.kilo;
+    cost = FDIV(cost * k.slot, k.mph);
+    cost = cost * k.kilo;
     // RLAgent.get_reward agent.py:225-232 (pre-update T_in)
-    float pen = fmaxf(fmaxf(0.0f, p.lower - tin), fmaxf(0.0f, tin - p.upper));
+    float pen = fmaxf(fmaxf(0.0f, k.lower - tin), fmaxf(0.0f, tin - k.upper));
     pen = pen > 0.0f ? pen + 1.0f : 0.0f;
-    const float rw = -(cost + p.penw * pen);
+    const float rw = -(cost + k.penw * pen);
 
     if (train && active) {
       // QAgent.train agent.py:293-298 -> QActor.train rl.py:119-129
       const uint32_t srow = st.strip + ip;
-      const QT qnew = td_update(rowR.v[act], rw, max3(rowN), p.alpha, p.gamma);
+      const QT qnew = td_update(sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]), rw, max3(rowN), k.alpha, k.gamma);
       q[srow * kQPad + act] = qnew;
       pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
     }
-    if (active) {
-      const size_t k = tA + a;
-      if (p.record & 1) p.rec_reward[k] = rw;
-      if (p.record & 2) p.rec_cost[k] = cost;
-      if (p.record & 4) p.rec_grid[k] = g;
-      if (p.record & 8) p.rec_p2p[k] = pp;
-      if (p.record & 16) p.rec_tin[k] = tin;
+    if (active && (rec & 31u)) {
+      if (rec & 1u) rec_reward[tA] = rw;
+      if (rec & 2u) rec_cost[tA] = cost;
+      if (rec & 4u) rec_grid[tA] = g;
+      if (rec & 8u) rec_p2p[tA] = pp;
+      if (rec & 16u) rec_tin[tA] = tin;
     }
     // avg_reward = sum_t mean_i r (community.py:179), canonical sequential order
     const float m = group_sum<N>(rw, lane, i, sl, shR);
@@ -486,6 +583,7 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
     f1 = f2;
     e2o = adv(e2o, env_step, env_end);
     f2o = adv(f2o, A, prof_end);
+    c1o = (t + 2 >= T) ? (size_t)0 : c1o + code_step;
     st = st1;
     cw = cw1;
     a0 = a0n;

@@ -1,0 +1,7 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -q -m gpu -x -rf > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest exit $rc"; tail -5 gpurun_out/gpu_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 600 python scripts/latency_ablation.py 2>&1 | tail -12
