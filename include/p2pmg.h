@@ -105,6 +105,11 @@ typedef struct p2pmg_config {
   int64_t scenario_offset; /* global index of this context's scenario 0 (multi-GPU sharding):
                               Philox counters use global agent ids so results do not depend
                               on how scenarios are split over ranks */
+  int32_t shared_q;        /* 0: one table per agent (the reference, rl.py:73);
+                              1: one shared policy table for every agent of every scenario
+                              (config 3, build-defined): frozen during an episode, TD deltas summed
+                              in int64 fixed point (2^-40) and applied by p2pmg_apply_q_delta */
+  int32_t reserved0;
 } p2pmg_config;
 
 typedef struct p2pmg_episode_args {
@@ -165,6 +170,27 @@ int p2pmg_reset_kernel_times(p2pmg_ctx* ctx);
 int p2pmg_rc_step(p2pmg_ctx* ctx, int n, const float* t_out, const float* t_in, const float* t_m,
                   const float* hp, float* t_in_new, float* t_m_new);
 int p2pmg_state_indices(p2pmg_ctx* ctx, int n, const float* obs /* [n][4] */, int32_t* idx /* [n][4] */);
+
+/* heterogeneous agents and storage (configs 3-4) */
+int p2pmg_set_hp_levels(p2pmg_ctx* ctx, const float* levels /* [A][3] W per action */);
+/* Battery per agent (storage.py:36-76, rule agent.py:138-153, f64): capacity [A] in J (0 = none;
+ * NULL disables storage), SoC bounds, round-trip efficiency, initial SoC [A] (NULL = 0.5). */
+int p2pmg_set_battery(p2pmg_ctx* ctx, const double* capacity, double min_soc, double max_soc,
+                      double efficiency, const double* soc0);
+int p2pmg_get_soc(p2pmg_ctx* ctx, double* soc);
+int p2pmg_battery_seq(p2pmg_ctx* ctx, int agents, int steps, const double* balance /* [agents][steps] */,
+                      double* out_balance, double* soc_hist, double* soc /* [agents] in/out */,
+                      const double* capacity, double min_soc, double max_soc, double efficiency);
+
+/* shared policy table (config.shared_q = 1) */
+int p2pmg_apply_q_delta(p2pmg_ctx* ctx);            /* Q += delta * 2^-40; delta = 0 */
+int p2pmg_get_q_delta(p2pmg_ctx* ctx, int64_t* host); /* [n_states][n_actions] fixed point */
+
+/* multi-GPU exchange of the shared-table deltas over RCCL (xGMI), loaded at run time */
+int p2pmg_comm_unique_id(uint8_t id[128]);
+int p2pmg_comm_init(p2pmg_ctx* ctx, const uint8_t id[128], int rank, int nranks);
+int p2pmg_allreduce_q_delta(p2pmg_ctx* ctx);        /* int64 sum over ranks, in place, on the stream */
+int p2pmg_comm_destroy(p2pmg_ctx* ctx);
 
 /* Standalone QActor calls (rl.py:89-129) on the context's per-agent tables, applied IN ORDER
  * by one device thread: for entry k, s = indices(s_obs[k]); a = codes[k] == P2PMG_GREEDY ?

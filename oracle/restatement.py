@@ -218,6 +218,28 @@ def temperature_step(t_out, t_in, t_m, hp, p: OracleParams = OracleParams()):
     return (t_in + (d_in * spm) * slot).astype(F32), (t_m + (d_m * spm) * slot).astype(F32)
 
 
+DELTA_SCALE = 2.0 ** 40  # shared-table TD deltas in int64 fixed point (build-defined)
+
+
+def battery_rule(balance, soc, cap, smin=0.1, smax=0.9, sqrt_eff=np.sqrt(0.9)):
+    """RuleAgent._update_storage (agent.py:138-153) with BatteryStorage (storage.py:79-100), f64,
+    vectorised; agents with cap == 0 are untouched.  Returns (balance', soc')."""
+    b = np.asarray(balance, np.float64)
+    soc = np.asarray(soc, np.float64)
+    cap = np.broadcast_to(np.asarray(cap, np.float64), b.shape)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        energy = (b * 60.0) * 15.0
+        avail_e = (np.maximum(0.0, soc - smin) * cap) * sqrt_eff
+        avail_s = (np.maximum(0.0, smax - soc) * cap) / sqrt_eff
+        dis = (b > 0) & (avail_e > 0) & (cap > 0)
+        chg = ~dis & (b < 0) & ~(soc >= smax) & (cap > 0)
+        xd = np.where(energy <= avail_e, energy, avail_e)
+        xc = np.where(-energy <= avail_s, -energy, avail_s)
+        soc2 = np.where(dis, soc - (xd / cap) / sqrt_eff, np.where(chg, soc + sqrt_eff * (xc / cap), soc))
+        b2 = np.where(dis, b - xd / 900.0, np.where(chg, b + xc / 900.0, b))
+    return b2, soc2
+
+
 # ----------------------------------------------------------------------------- RNG replay
 def reference_replay_codes(rs: np.random.RandomState, T: int, R: int, N: int, eps) -> np.ndarray:
     """Exploration draws in the reference's exact consumption order:
@@ -255,6 +277,10 @@ class OracleBatch:
     q_dtype: str = "f64"
     params: OracleParams = field(default_factory=OracleParams)
     price_table: Optional[tuple] = None  # (buy, inj, p2p) [S_env, T] f32; default: prices()
+    shared_q: bool = False               # one frozen policy table, int64 fixed-point deltas
+    hp_levels: Optional[np.ndarray] = None  # [S, N, 3] f32 per-agent heat-pump power per action
+    battery_capacity: Optional[np.ndarray] = None  # [S, N] J (0 = none); None = no storage
+    battery_bounds: tuple = (0.1, 0.9, 0.9)        # (min_soc, max_soc, efficiency)
 
     def __post_init__(self):
         p = self.params
@@ -266,7 +292,12 @@ class OracleBatch:
         self.env_tout = np.asarray(self.env_tout, dtype=F32).reshape(-1, self.T)
         self.n_states = p.n_time * p.n_temp * p.n_bal * p.n_p2p
         qt = np.float64 if self.q_dtype == "f64" else np.float32
-        self.q = np.zeros((self.S * self.N, self.n_states, p.n_actions), dtype=qt)
+        self.q = np.zeros((1 if self.shared_q else self.S * self.N, self.n_states, p.n_actions), dtype=qt)
+        self.q_delta = np.zeros((self.n_states, p.n_actions), np.int64)
+        if self.hp_levels is None:
+            self.hp_levels = np.broadcast_to(p.hp_levels, (self.S, self.N, 3)).astype(F32)
+        self.hp_levels = np.asarray(self.hp_levels, F32).reshape(self.S, self.N, 3)
+        self.soc = np.full((self.S, self.N), 0.5)
         self.t_in = np.full((self.S, self.N), F32(p.setpoint), dtype=F32)
         self.t_m = np.full((self.S, self.N), F32(p.setpoint), dtype=F32)
         if self.price_table is None:
@@ -282,6 +313,13 @@ class OracleBatch:
 
     def set_q_table(self, agent: int, table: np.ndarray):
         self.q[agent] = np.asarray(table).reshape(self.n_states, -1).astype(self.q.dtype)
+
+    def apply_q_delta(self):
+        """Shared table: Q += delta * 2^-40 (f64) where delta != 0; delta = 0."""
+        nz = self.q_delta != 0
+        q0 = self.q[0]
+        q0[nz] = (q0[nz].astype(np.float64) + self.q_delta[nz].astype(np.float64) * (1.0 / DELTA_SCALE)).astype(q0.dtype)
+        self.q_delta[:] = 0
 
     def _env(self, arr, t):
         return arr[:, t] if arr.shape[0] == self.S else np.broadcast_to(arr[0, t], (self.S,))
@@ -300,7 +338,13 @@ class OracleBatch:
         A = S * N
         agents = np.arange(A).reshape(S, N)
         gids = agents if agent_ids is None else np.asarray(agent_ids).reshape(S, N)  # Philox counters
-        lv = p.hp_levels
+        tab = np.zeros_like(agents) if self.shared_q else agents  # which Q table each agent reads
+        lv = self.hp_levels
+        bat = self.battery_capacity is not None
+        if bat:
+            cap = np.asarray(self.battery_capacity, np.float64).reshape(S, N)
+            smin, smax, eff = self.battery_bounds
+            sqe = np.sqrt(eff)
         mi = self.max_in
         eps_arr = np.broadcast_to(np.asarray(eps, dtype=np.float64), (S, N))
         tr = {k: [] for k in ("action", "idx", "reward", "cost", "grid", "p2p", "t_in", "t_m", "hp")}
@@ -325,6 +369,7 @@ class OracleBatch:
             acts = np.zeros((R + 1, S, N), dtype=np.int64)
             idxs = np.zeros((R + 1, S, N, 4), dtype=np.int64)
             hp = np.zeros((S, N), dtype=F32)
+            soc_r = self.soc.copy() if bat else None
             for r in range(R + 1):
                 # P <- P - diag(diag(P))  community.py:76
                 d = np.arange(N)
@@ -333,7 +378,7 @@ class OracleBatch:
                 p2pf = (seq_sum(powers) / F32(N)) / mi  # agent.py:203
                 ip = state_index(p2pf, p.n_p2p, "plain")
                 row = self._row(it, iT, ib, ip)
-                qrow = self.q[agents, row]  # (S, N, 3)
+                qrow = self.q[tab, row]  # (S, N, 3)
                 greedy = np.argmax(qrow, axis=-1)  # first max wins (rl.py:116)
                 if mode == "greedy":
                     a = greedy
@@ -345,11 +390,16 @@ class OracleBatch:
                     u = u.reshape(S, N)
                     ra = ra.reshape(S, N)
                     a = np.where(u < eps_arr, ra, greedy)
-                hp = lv[a]
+                hp = np.take_along_axis(lv, a[..., None], axis=-1)[..., 0]
                 out = (bal * mi) + hp  # agent.py:210
+                if bat:  # battery rule on the net power, SoC committed by the final round
+                    ob_, soc_r = battery_rule(out.astype(np.float64), self.soc, cap, smin, smax, sqe)
+                    out = np.where(cap > 0, ob_.astype(F32), out).astype(F32)
                 P = divide_power(out, powers, N)  # rows stacked after all agents (Jacobi)
                 acts[r] = a
                 idxs[r] = np.stack([it, iT, ib, ip], axis=-1)
+            if bat:
+                self.soc = soc_r
             g, pp = assign_powers(P)
             cost = compute_costs(g, pp, buy[:, None], inj[:, None], p2pp[:, None], p)
             rew = reward(cost, self.t_in, p)
@@ -359,15 +409,19 @@ class OracleBatch:
                 ibn = state_index(baln, p.n_bal, "plain")
                 ipn = state_index(np.zeros((S, N), F32) / mi, p.n_p2p, "plain")
                 nrow = self._row(itn, iT, ibn, ipn)
-                qmax = self.q[agents, nrow].max(axis=-1)
+                qmax = self.q[tab, nrow].max(axis=-1)
                 srow = self._row(it, iT, ib, idxs[R][..., 3])
                 a = acts[R]
-                qsa = self.q[agents, srow, a]
-                if qf is np.float64:
+                qsa = self.q[tab, srow, a]
+                if self.shared_q:
+                    d = p.alpha * ((rew.astype(np.float64) + p.gamma * qmax.astype(np.float64)) - qsa.astype(np.float64))
+                    np.add.at(self.q_delta, (srow.ravel(), a.ravel()), np.rint(d * DELTA_SCALE).astype(np.int64).ravel())
+                elif qf is np.float64:
                     new = qsa + p.alpha * ((rew.astype(np.float64) + p.gamma * qmax) - qsa)
                 else:
                     new = qsa + F32(p.alpha) * ((rew + F32(p.gamma) * qmax) - qsa)
-                self.q[agents, srow, a] = new
+                if not self.shared_q:
+                    self.q[agents, srow, a] = new
             tr["action"].append(acts)
             tr["idx"].append(idxs)
             tr["reward"].append(rew)

@@ -28,7 +28,9 @@ EXPORTS = [
     "p2pmg_set_replay_codes", "p2pmg_zero_q", "p2pmg_set_q", "p2pmg_get_q", "p2pmg_run_episode",
     "p2pmg_get_record", "p2pmg_get_episode_reward", "p2pmg_last_kernel_ms", "p2pmg_rc_step",
     "p2pmg_state_indices", "p2pmg_replay_decode", "p2pmg_device_count", "p2pmg_kernel_times",
-    "p2pmg_reset_kernel_times", "p2pmg_q_calls",
+    "p2pmg_reset_kernel_times", "p2pmg_q_calls", "p2pmg_set_hp_levels", "p2pmg_set_battery", "p2pmg_get_soc",
+    "p2pmg_battery_seq", "p2pmg_apply_q_delta", "p2pmg_get_q_delta", "p2pmg_comm_unique_id", "p2pmg_comm_init",
+    "p2pmg_allreduce_q_delta", "p2pmg_comm_destroy",
 ]
 
 
@@ -43,7 +45,7 @@ class Config(C.Structure):
         ("inv_rvent", C.c_float), ("one_minus_frad", C.c_float), ("frad", C.c_float), ("solar_gain", C.c_float),
         ("hp_cop", C.c_float), ("seconds_per_minute", C.c_float), ("time_slot", C.c_float),
         ("minutes_per_hour", C.c_float), ("kilo", C.c_float), ("penalty_weight", C.c_float),
-        ("seed", C.c_uint64), ("scenario_offset", C.c_int64),
+        ("seed", C.c_uint64), ("scenario_offset", C.c_int64), ("shared_q", C.c_int32), ("reserved0", C.c_int32),
     ]
 
 
@@ -96,6 +98,16 @@ def _declare(lib):
         "p2pmg_kernel_times": ([vp, fp, i32, C.POINTER(C.c_int)], i32),
         "p2pmg_reset_kernel_times": ([vp], i32),
         "p2pmg_q_calls": ([vp, i32, vp, vp, vp, vp, vp, i32, vp, vp], i32),
+        "p2pmg_set_hp_levels": ([vp, fp], i32),
+        "p2pmg_set_battery": ([vp, vp, C.c_double, C.c_double, C.c_double, vp], i32),
+        "p2pmg_get_soc": ([vp, vp], i32),
+        "p2pmg_battery_seq": ([vp, i32, i32, vp, vp, vp, vp, vp, C.c_double, C.c_double, C.c_double], i32),
+        "p2pmg_apply_q_delta": ([vp], i32),
+        "p2pmg_get_q_delta": ([vp, vp], i32),
+        "p2pmg_comm_unique_id": ([vp], i32),
+        "p2pmg_comm_init": ([vp, vp, i32, i32], i32),
+        "p2pmg_allreduce_q_delta": ([vp], i32),
+        "p2pmg_comm_destroy": ([vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

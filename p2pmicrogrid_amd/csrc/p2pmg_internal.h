@@ -11,6 +11,7 @@ constexpr int kQPad = 4;       // Q row padded to 4 actions: 32-B (f64) / 16-B (
 constexpr int kWave = 64;      // one wave per workgroup
 constexpr int kMaxAgents = 16; // compiled-in agents per scenario
 constexpr int kMaxRounds1 = 8; // R + 1 <= 8 (two code words)
+constexpr double kDeltaScale = 1099511627776.0;  // 2^40: shared-table TD deltas in int64 fixed point
 
 // Everything the episode kernel needs, passed by value in the kernarg segment.
 struct EpisodeParams {
@@ -35,6 +36,16 @@ struct EpisodeParams {
   uint8_t* rec_action;       // [T][R+1][A]
   int32_t* rec_index;        // [T][R+1][A]
   float* ep_reward;          // [S]
+  // shared policy (config 3): every agent reads one frozen table; TD deltas accumulate in
+  // int64 fixed point (2^-40) with device atomics, applied at episode end (p2pmg_apply_q_delta)
+  int shared_q;
+  long long* qdelta;         // [n_states][kQPad] int64
+  // battery (agent.py:138-153 rule, storage.py:36-76 bookkeeping), f64 like the reference
+  int battery;
+  double* soc;               // [A] in/out
+  const double* bat_cap;     // [A] capacity in J (0 = no battery)
+  double bat_min, bat_max, bat_sqrt_eff;
+  const float4* hp_lv;       // [A] per-agent heat-pump power of actions 0..2 (agent.py:268, heating.py:124)
   int nt, nT, nb, np;
   double alpha, gamma;
   float hp_levels[4];
@@ -48,6 +59,10 @@ struct RcParams {
 };
 
 hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream);
+hipError_t launch_apply_delta(void* q, long long* qdelta, size_t n, int q_dtype, hipStream_t stream);
+hipError_t launch_battery_seq(int agents, int steps, const double* bal, double* out_bal, double* soc_hist,
+                              double* soc, const double* cap, double smin, double smax, double sqrt_eff,
+                              hipStream_t stream);
 hipError_t launch_philox_codes(const EpisodeParams& p, uint32_t* words, hipStream_t stream);
 hipError_t launch_pack_codes(int T, int R1, int A, const uint8_t* in, uint32_t* words, hipStream_t stream);
 hipError_t launch_rc_step(int n, const float* t_out, const float* t_in, const float* t_m, const float* hp,

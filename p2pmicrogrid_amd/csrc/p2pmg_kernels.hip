@@ -146,6 +146,25 @@ __device__ __forceinline__ float td_update(float qsa, float rw, float qmax, doub
   return qsa + (float)alpha * ((rw + (float)gamma * qmax) - qsa);
 }
 
+// RuleAgent._update_storage (agent.py:138-153) with BatteryStorage bookkeeping (storage.py:79-100),
+// f64 like the reference's Python floats.  Returns the adjusted balance (W); soc is updated.
+__device__ __forceinline__ double battery_rule(double balance, double& soc, double cap, double smin, double smax,
+                                               double sqrt_eff) {
+  const double energy = (balance * 60.0) * 15.0;
+  const double avail_energy = (fmax(0.0, soc - smin) * cap) * sqrt_eff;
+  const double avail_space = (fmax(0.0, smax - soc) * cap) / sqrt_eff;
+  if (balance > 0.0 && avail_energy > 0.0) {
+    const double x = energy <= avail_energy ? energy : avail_energy;  // min(energy, available_energy)
+    soc = soc - (x / cap) / sqrt_eff;
+    balance = balance - x / 900.0;
+  } else if (balance < 0.0 && !(soc >= smax)) {
+    const double x = -energy <= avail_space ? -energy : avail_space;
+    soc = soc + sqrt_eff * (x / cap);
+    balance = balance + x / 900.0;
+  }
+  return balance;
+}
+
 // ----------------------------------------------------------------- scenario-group exchange
 // Lane i of a scenario group owns row i of the proposal matrix P.  exchange() gives every lane
 // its column: col[j] = P[j][i].  G <= 8: cross-lane shuffles (no LDS, no barrier — a
@@ -268,7 +287,7 @@ __device__ __forceinline__ double vpin(double x) {
 struct KC {
   float setpoint, margin, lower, upper;
   float inv_ci, inv_cm, inv_ri, inv_re, inv_rvent, c_in, c_m, solar, cop, spm, slot;
-  float mph, kilo, penw, l0, l1, l2;
+  float mph, kilo, penw;
   double alpha, gamma;
   int nt, nT, nb, np;
 };
@@ -278,7 +297,7 @@ __device__ __forceinline__ KC pin_constants(const EpisodeParams& p) {
   k.inv_ci = vpin(p.inv_ci); k.inv_cm = vpin(p.inv_cm); k.inv_ri = vpin(p.inv_ri); k.inv_re = vpin(p.inv_re);
   k.inv_rvent = vpin(p.inv_rvent); k.c_in = vpin(p.c_in); k.c_m = vpin(p.c_m); k.solar = vpin(p.solar);
   k.cop = vpin(p.cop); k.spm = vpin(p.spm); k.slot = vpin(p.slot); k.mph = vpin(p.mph); k.kilo = vpin(p.kilo);
-  k.penw = vpin(p.penw); k.l0 = vpin(p.hp_levels[0]); k.l1 = vpin(p.hp_levels[1]); k.l2 = vpin(p.hp_levels[2]);
+  k.penw = vpin(p.penw);
   k.alpha = vpin(p.alpha); k.gamma = vpin(p.gamma);
   k.nt = vpin(p.nt); k.nT = vpin(p.nT); k.nb = vpin(p.nb); k.np = vpin(p.np);
   return k;
@@ -292,20 +311,32 @@ struct StepIdx {
   uint32_t strip;   // row of (it, iT, ib, 0) in the agent's table
   uint32_t nrow;    // next-state row (time_{t+1}, same T_in, bal_{t+1}, p2p = 0)  agent.py:293-296
 };
-__device__ __forceinline__ StepIdx make_step(const KC& p, bool margin_one, float time_t, float time_n, float bal,
-                                             float2 f_n, float tin, float mi, int ip_zero) {
+// Q-table dimensions: the reference's 20 x 20 x 20 x 20 (agent.py:258-261) compile to shifts and
+// adds; other sizes use the runtime values
+template <bool B20>
+struct Dims {
+  int nt, nT, nb, np;
+  __device__ __forceinline__ int t() const { return B20 ? 20 : nt; }
+  __device__ __forceinline__ int T() const { return B20 ? 20 : nT; }
+  __device__ __forceinline__ int b() const { return B20 ? 20 : nb; }
+  __device__ __forceinline__ int p() const { return B20 ? 20 : np; }
+};
+
+template <bool B20>
+__device__ __forceinline__ StepIdx make_step(const KC& p, const Dims<B20>& D, bool margin_one, float time_t,
+                                             float time_n, float bal, float2 f_n, float tin, float mi, int ip_zero) {
   StepIdx st;
   st.bal = bal;
   st.baln = FDIV(f_n.x - f_n.y, mi);
   const float dt = tin - p.setpoint;  // heating.py:118-120 (x / 1.0 == x exactly)
   const float tnorm = margin_one ? dt : dt / p.margin;
-  st.it = idx_time(time_t, p.nt);
-  st.iT = idx_temp(tnorm, p.nT);
-  st.ib = idx_plain(bal, p.nb);
-  st.strip = (uint32_t)(((st.it * p.nT + st.iT) * p.nb + st.ib) * p.np);
-  const int itn = idx_time(time_n, p.nt);
-  const int ibn = idx_plain(st.baln, p.nb);
-  st.nrow = (uint32_t)(((itn * p.nT + st.iT) * p.nb + ibn) * p.np + ip_zero);
+  st.it = idx_time(time_t, D.t());
+  st.iT = idx_temp(tnorm, D.T());
+  st.ib = idx_plain(bal, D.b());
+  st.strip = (uint32_t)(((st.it * D.T() + st.iT) * D.b() + st.ib) * D.p());
+  const int itn = idx_time(time_n, D.t());
+  const int ibn = idx_plain(st.baln, D.b());
+  st.nrow = (uint32_t)(((itn * D.T() + st.iT) * D.b() + ibn) * D.p() + ip_zero);
   return st;
 }
 
@@ -367,7 +398,7 @@ __device__ __forceinline__ Row4<QT> patched(Row4<QT> r, uint32_t addr, const Pat
 
 // heat-pump power of an action without a dynamically indexed kernarg array (that compiles to
 // a global load + vmcnt(0) on the critical path)
-__device__ __forceinline__ float hp_of(const KC& k, int act) { return sel3(act, k.l0, k.l1, k.l2); }
+__device__ __forceinline__ float hp_of(const float4& lv, int act) { return sel3(act, lv.x, lv.y, lv.z); }
 
 // ----------------------------------------------------------------- the episode kernel
 // One launch = one episode of T timesteps for every scenario (train_episode / run).
@@ -386,7 +417,7 @@ __device__ __forceinline__ Row4<QT> gather_row(const QT* p) {
   return load_row(p);
 #endif
 }
-template <int N, typename QT>
+template <int N, typename QT, bool B20>
 __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   constexpr int G = pow2ceil(N);
   constexpr int SPW = kWave / G;
@@ -409,14 +440,20 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   const uint32_t rec = (uint32_t)p.record;
   const size_t A = (size_t)p.A;
   const KC k = pin_constants(p);  // loop constants in VGPRs (no SGPR spill reloads on the chain)
+  const Dims<B20> D{k.nt, k.nT, k.nb, k.np};
 
   const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
-  QT* __restrict__ q = reinterpret_cast<QT*>(p.q) + (size_t)a * n_states * kQPad;
+  const bool shared = p.shared_q != 0;
+  QT* __restrict__ q = reinterpret_cast<QT*>(p.q) + (shared ? (size_t)0 : (size_t)a * n_states * kQPad);
   const float mi = active ? p.max_in[a] : 1.0f;
+  const float4 lv = p.hp_lv[a];  // heat-pump power of actions 0..2 for this agent
+  const bool bat = p.battery != 0;
+  const double bcap = bat ? p.bat_cap[a] : 0.0;
+  double soc = bat ? p.soc[a] : 0.0;
   float tin = active ? p.t_in[a] : k.setpoint;
   float tm = active ? p.t_m[a] : k.setpoint;
   // round 0 and the next state both have p2p = mean(-0 ... -0) / max_in = 0 (agent.py:203, community.py:161)
-  const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, k.np);
+  const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, D.p());
 
   // running offsets (no 64-bit multiplies in the loop)
   const float* envb = p.env + (size_t)s_env * kEnvStride;
@@ -443,7 +480,7 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   EnvRow e1 = load_env(envb + e1o);
   const float2 f0 = prof_at(0);
   float2 f1 = prof_at(f1o);
-  StepIdx st = make_step(k, margin_one, e0.time, e1.time, FDIV(f0.x - f0.y, mi), f1, tin, mi, ip_zero);
+  StepIdx st = make_step(k, D, margin_one, e0.time, e1.time, FDIV(f0.x - f0.y, mi), f1, tin, mi, ip_zero);
   uint64_t cw = code_word(p, step_codes(p, codes_a, 0, 0, a, W), active);
   // Q rows are loaded unconditionally (a load under a divergent branch is waited for at the
   // join, which would serialise the prefetch); a row that is not needed aliases one that is
@@ -477,6 +514,7 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
     for (int j = 0; j < N; ++j) { row[j] = 0.0f; col[j] = 0.0f; }
     int act = 0, ip = ip_zero;
     float hp = 0.0f;
+    double soc_r = soc;  // tentative SoC of the current round
     row0 = patched(row0, a0, pat);  // the previous step's TD store may have hit a prefetched row
     rowN = patched(rowN, aN, pat);
     Row4<QT> rowR = row0;  // Q row of the final round's state (TD target Q[s, a])
@@ -489,16 +527,21 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
         float acc = 0.0f;
 #pragma unroll
         for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : col[j]));
-        ip = idx_plain(FDIV(div_n<N>(acc), mi), k.np);
+        ip = idx_plain(FDIV(div_n<N>(acc), mi), D.p());
         // the final round's row is needed for the TD update even when exploring
         const bool need = code == 255 || (train && r == R1 - 1);
         rowR = gather_row(q + (need ? st.strip + (uint32_t)ip : a0) * kQPad);
       }
       act = code == 255 ? argmax3(rowR) : code;  // QAgent._act / take_decision (agent.py:271-289)
-      hp = hp_of(k, act);
+      hp = hp_of(lv, act);
 
-      // RLAgent._divide_power agent.py:186-195 on out = bal * max_in + hp (agent.py:210)
-      const float out = (st.bal * mi) + hp;
+      // RLAgent._divide_power agent.py:186-195 on out = bal * max_in + hp (agent.py:210);
+      // with a battery the rule adjusts the net power first (SoC committed by the last round)
+      float out = (st.bal * mi) + hp;
+      if (bat && bcap > 0.0) {
+        soc_r = soc;
+        out = (float)battery_rule((double)out, soc_r, bcap, p.bat_min, p.bat_max, p.bat_sqrt_eff);
+      }
       const float so = sgn(out);
       float f[N];
       float tot = 0.0f;
@@ -514,8 +557,9 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
 #pragma unroll
         for (int j = 0; j < N; ++j) row[j] = ev;
       } else {
+        // |f_ii| = 0 (own power is -0): (out * 0) / tot == out * 0 exactly for any non-NaN tot
 #pragma unroll
-        for (int j = 0; j < N; ++j) row[j] = FDIV(out * fabsf(f[j]), tot);
+        for (int j = 0; j < N; ++j) row[j] = (j == i) ? (tot == tot ? out * 0.0f : tot) : FDIV(out * fabsf(f[j]), tot);
       }
       if (active && (rec & 96u)) {
         const size_t kk = (tA * R1) + (size_t)r * A;
@@ -524,12 +568,13 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
       }
     }
 
+    soc = soc_r;  // BatteryStorage state after the final round's decision
     // CommunityMicrogrid._step -> HPHeating.step (community.py:184-188, heating.py:138-143):
     // computed now so the next step's rows can be issued before this step's market work
     float tin1 = tin, tm1 = tm;
     rc_update(k, e0.t_out, hp, tin1, tm1);
     // (after the last step this prefetches a wrapped, unused step: harmless valid addresses)
-    const StepIdx st1 = make_step(k, margin_one, e1.time, e2.time, st.baln, f2, tin1, mi, ip_zero);
+    const StepIdx st1 = make_step(k, D, margin_one, e1.time, e2.time, st.baln, f2, tin1, mi, ip_zero);
     const uint64_t cw1 = code_word(p, cw1r, active);
     const uint32_t a0n = row0_addr(st1, cw1);
     const uint32_t aNn = train ? st1.nrow : a0n;
@@ -561,9 +606,18 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
     if (train && active) {
       // QAgent.train agent.py:293-298 -> QActor.train rl.py:119-129
       const uint32_t srow = st.strip + ip;
-      const QT qnew = td_update(sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]), rw, max3(rowN), k.alpha, k.gamma);
-      q[srow * kQPad + act] = qnew;
-      pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
+      const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
+      if (shared) {
+        // frozen shared table: delta = alpha * ((r + gamma * max Q[ns]) - Q[s, a]) in f64, summed in
+        // int64 fixed point (order-independent, so every launch and every rank sums identically)
+        const double d = k.alpha * (((double)rw + k.gamma * (double)max3(rowN)) - (double)qsa);
+        atomicAdd(reinterpret_cast<unsigned long long*>(p.qdelta) + (size_t)srow * kQPad + act,
+                  (unsigned long long)__double2ll_rn(d * kDeltaScale));
+      } else {
+        const QT qnew = td_update(qsa, rw, max3(rowN), k.alpha, k.gamma);
+        q[srow * kQPad + act] = qnew;
+        pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
+      }
     }
     if (active && (rec & 31u)) {
       if (rec & 1u) rec_reward[tA] = rw;
@@ -594,8 +648,36 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   if (active) {
     p.t_in[a] = tin;
     p.t_m[a] = tm;
+    if (bat) p.soc[a] = soc;
     if (i == 0) p.ep_reward[s] = ep_sum;
   }
+}
+
+// Q += delta * 2^-40 (f64), delta = 0: the end-of-episode update of the shared table, after the
+// optional all-reduce of the int64 deltas over ranks
+template <typename QT>
+__global__ void apply_delta_kernel(QT* __restrict__ q, long long* __restrict__ d, size_t n) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const long long x = d[k];
+  if (x != 0) {
+    q[k] = (QT)((double)q[k] + (double)x * (1.0 / kDeltaScale));
+    d[k] = 0;
+  }
+}
+
+// battery rule over per-agent sequences (unit parity with storage.py / agent.py:138-153)
+__global__ void battery_seq_kernel(int agents, int steps, const double* bal, double* out_bal, double* soc_hist,
+                                   double* soc, const double* cap, double smin, double smax, double sqrt_eff) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= agents) return;
+  double s_ = soc[a];
+  for (int t = 0; t < steps; ++t) {
+    const size_t k = (size_t)a * steps + t;
+    out_bal[k] = battery_rule(bal[k], s_, cap[a], smin, smax, sqrt_eff);
+    soc_hist[k] = s_;
+  }
+  soc[a] = s_;
 }
 
 // Philox pre-pass: every (t, agent) code word of an episode in one parallel launch, so the
@@ -635,7 +717,10 @@ template <int N, typename QT>
 hipError_t launch_n(const EpisodeParams& p, hipStream_t st) {
   constexpr int SPW = kWave / pow2ceil(N);
   const int blocks = (p.S + SPW - 1) / SPW;
-  hipLaunchKernelGGL((episode_kernel<N, QT>), dim3(blocks), dim3(kWave), 0, st, p);
+  if (p.nt == 20 && p.nT == 20 && p.nb == 20 && p.np == 20)
+    hipLaunchKernelGGL((episode_kernel<N, QT, true>), dim3(blocks), dim3(kWave), 0, st, p);
+  else
+    hipLaunchKernelGGL((episode_kernel<N, QT, false>), dim3(blocks), dim3(kWave), 0, st, p);
   return hipGetLastError();
 }
 
@@ -751,6 +836,23 @@ hipError_t launch_pack_codes(int T, int R1, int A, const uint8_t* in, uint32_t* 
   const size_t n = (size_t)T * A;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(pack_codes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, T, R1, A, in, words);
+  return hipGetLastError();
+}
+
+hipError_t launch_apply_delta(void* q, long long* qdelta, size_t n, int q_dtype, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if (q_dtype == 0)
+    hipLaunchKernelGGL(apply_delta_kernel<double>, dim3(grid_for(n, 256)), dim3(256), 0, stream, (double*)q, qdelta, n);
+  else
+    hipLaunchKernelGGL(apply_delta_kernel<float>, dim3(grid_for(n, 256)), dim3(256), 0, stream, (float*)q, qdelta, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_battery_seq(int agents, int steps, const double* bal, double* out_bal, double* soc_hist, double* soc,
+                              const double* cap, double smin, double smax, double sqrt_eff, hipStream_t stream) {
+  if (agents <= 0) return hipSuccess;
+  hipLaunchKernelGGL(battery_seq_kernel, dim3(grid_for(agents, 64)), dim3(64), 0, stream, agents, steps, bal, out_bal,
+                     soc_hist, soc, cap, smin, smax, sqrt_eff);
   return hipGetLastError();
 }
 

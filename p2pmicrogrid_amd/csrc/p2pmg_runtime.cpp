@@ -3,6 +3,7 @@
 // returns a status and records a message in the context.
 #include "p2pmg.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -44,9 +45,50 @@ struct p2pmg_ctx {
   float* rec_f32[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // reward, cost, grid, p2p, tin
   uint8_t* rec_action = nullptr;
   int32_t* rec_index = nullptr;
+  float4* hp_lv = nullptr;     // [A] per-agent heat-pump levels
+  double* soc = nullptr;       // [A]
+  double* bat_cap = nullptr;   // [A]
+  bool battery = false;
+  double bat_min = 0.1, bat_max = 0.9, bat_sqrt_eff = 1.0;
+  long long* qdelta = nullptr; // shared table deltas [n_states][4]
+  void* comm = nullptr;        // ncclComm_t
   bool have_env = false, have_prof = false, have_params = false, have_codes = false;
   std::string err;
 };
+
+// ---- RCCL, resolved at run time (torch may already have loaded its own librccl; dlopen by
+// SONAME then reuses it, and the library stays loadable on hosts without RCCL)
+struct Id128 {  // ncclUniqueId, passed by value to ncclCommInitRank
+  char b[128];
+};
+struct Rccl {
+  void* h = nullptr;
+  int (*getUniqueId)(void*) = nullptr;
+  int (*commInitRank)(void**, int, Id128, int) = nullptr;
+  int (*allReduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;  // ncclDataType_t, ncclRedOp_t as int
+  int (*commDestroy)(void*) = nullptr;
+  const char* (*getErrorString)(int) = nullptr;
+};
+static Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+    for (const char* n : names) {
+      r.h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+      if (r.h) break;
+    }
+    if (r.h) {
+      r.getUniqueId = (int (*)(void*))dlsym(r.h, "ncclGetUniqueId");
+      r.commInitRank = (int (*)(void**, int, Id128, int))dlsym(r.h, "ncclCommInitRank");
+      r.allReduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(r.h, "ncclAllReduce");
+      r.commDestroy = (int (*)(void*))dlsym(r.h, "ncclCommDestroy");
+      r.getErrorString = (const char* (*)(int))dlsym(r.h, "ncclGetErrorString");
+    }
+  }
+  return (r.h && r.getUniqueId && r.commInitRank && r.allReduce && r.commDestroy) ? &r : nullptr;
+}
 
 namespace {
 
@@ -186,8 +228,22 @@ int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
   const size_t ncw = (size_t)c->T * ((c->R + 4) / 4) * A;
   if (dmalloc(&c->codes, ncw) != hipSuccess) return bail(P2PMG_E_NOMEM);
   if (hipMemsetAsync(c->codes, 0xFF, ncw * 4, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
-  const size_t qbytes = A * c->n_states * kQPad * c->q_elem;
+  const size_t n_tables = cfg->shared_q ? 1 : A;
+  const size_t qbytes = n_tables * c->n_states * kQPad * c->q_elem;
   if (hipMalloc(&c->q, qbytes) != hipSuccess) return bail(P2PMG_E_NOMEM);
+  if (cfg->shared_q) {
+    if (dmalloc(&c->qdelta, c->n_states * kQPad) != hipSuccess) return bail(P2PMG_E_NOMEM);
+    if (hipMemsetAsync(c->qdelta, 0, c->n_states * kQPad * 8, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
+  }
+  if (dmalloc(&c->hp_lv, A) != hipSuccess || dmalloc(&c->soc, A) != hipSuccess) return bail(P2PMG_E_NOMEM);
+  {
+    std::vector<float4> lv(A, make_float4(cfg->hp_levels[0], cfg->hp_levels[1], cfg->hp_levels[2], 0.0f));
+    std::vector<double> s0(A, 0.5);
+    if (hipMemcpyAsync(c->hp_lv, lv.data(), A * sizeof(float4), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(c->soc, s0.data(), A * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+      return bail(P2PMG_E_HIP);
+  }
   if (hipMemsetAsync(c->q, 0, qbytes, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
   std::vector<float> t0(A, cfg->setpoint);
   if (hipMemcpyAsync(c->t_in, t0.data(), A * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
@@ -212,6 +268,12 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   for (auto& b : c->rec_f32) dfree(b);
   dfree(c->rec_action);
   dfree(c->rec_index);
+  dfree(c->hp_lv);
+  dfree(c->soc);
+  dfree(c->bat_cap);
+  dfree(c->qdelta);
+  if (c->comm && rccl()) rccl()->commDestroy(c->comm);
+  c->comm = nullptr;
   for (auto& ev : c->ring)
     if (ev) (void)hipEventDestroy(ev);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -344,12 +406,15 @@ int p2pmg_set_replay_codes(p2pmg_ctx* c, const uint8_t* codes) {
 
 int p2pmg_zero_q(p2pmg_ctx* c) {
   if (!c) return P2PMG_E_INVALID;
-  HIP_TRY(c, hipMemsetAsync(c->q, 0, (size_t)c->A * c->n_states * kQPad * c->q_elem, c->stream));
+  const size_t n_tables = c->cfg.shared_q ? 1 : (size_t)c->A;
+  HIP_TRY(c, hipMemsetAsync(c->q, 0, n_tables * c->n_states * kQPad * c->q_elem, c->stream));
+  if (c->qdelta) HIP_TRY(c, hipMemsetAsync(c->qdelta, 0, c->n_states * kQPad * 8, c->stream));
   return P2PMG_OK;
 }
 
 static int q_range_ok(p2pmg_ctx* c, int first, int count, const void* host, int dtype) {
-  if (!c || !host || first < 0 || count < 0 || first + count > c->A) return 0;
+  const int n_tables = c && c->cfg.shared_q ? 1 : (c ? c->A : 0);
+  if (!c || !host || first < 0 || count < 0 || first + count > n_tables) return 0;
   return dtype == P2PMG_Q_F64 || dtype == P2PMG_Q_F32;
 }
 
@@ -427,6 +492,15 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   p.rec_action = c->rec_action;
   p.rec_index = c->rec_index;
   p.ep_reward = c->ep_reward;
+  p.shared_q = g.shared_q ? 1 : 0;
+  p.qdelta = c->qdelta;
+  p.battery = c->battery ? 1 : 0;
+  p.soc = c->soc;
+  p.bat_cap = c->bat_cap;
+  p.bat_min = c->bat_min;
+  p.bat_max = c->bat_max;
+  p.bat_sqrt_eff = c->bat_sqrt_eff;
+  p.hp_lv = c->hp_lv;
   p.nt = g.n_time_states;
   p.nT = g.n_temp_states;
   p.nb = g.n_balance_states;
@@ -586,6 +660,122 @@ int p2pmg_state_indices(p2pmg_ctx* c, int n, const float* obs, int32_t* idx) {
   dfree(d);
   dfree(di);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("state_indices: ") + hipGetErrorString(e));
+  return P2PMG_OK;
+}
+
+int p2pmg_set_hp_levels(p2pmg_ctx* c, const float* levels) {
+  if (!c || !levels) return P2PMG_E_INVALID;
+  std::vector<float4> lv((size_t)c->A);
+  for (size_t a = 0; a < lv.size(); ++a) lv[a] = make_float4(levels[3 * a], levels[3 * a + 1], levels[3 * a + 2], 0.0f);
+  HIP_TRY(c, hipMemcpyAsync(c->hp_lv, lv.data(), lv.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_set_battery(p2pmg_ctx* c, const double* capacity, double min_soc, double max_soc, double efficiency,
+                      const double* soc0) {
+  if (!c) return P2PMG_E_INVALID;
+  if (!capacity) {
+    c->battery = false;
+    return P2PMG_OK;
+  }
+  if (!(efficiency > 0.0) || !(min_soc <= max_soc)) return fail(c, P2PMG_E_INVALID, "set_battery: bad parameters");
+  const size_t A = (size_t)c->A;
+  if (!c->bat_cap) HIP_TRY(c, dmalloc(&c->bat_cap, A));
+  HIP_TRY(c, hipMemcpyAsync(c->bat_cap, capacity, A * 8, hipMemcpyHostToDevice, c->stream));
+  std::vector<double> s0(A, 0.5);
+  HIP_TRY(c, hipMemcpyAsync(c->soc, soc0 ? soc0 : s0.data(), A * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->battery = true;
+  c->bat_min = min_soc;
+  c->bat_max = max_soc;
+  c->bat_sqrt_eff = std::sqrt(efficiency);  // np.sqrt(self.battery.efficiency), storage.py:86-100
+  return P2PMG_OK;
+}
+
+int p2pmg_get_soc(p2pmg_ctx* c, double* soc) {
+  if (!c || !soc) return P2PMG_E_INVALID;
+  HIP_TRY(c, hipMemcpyAsync(soc, c->soc, (size_t)c->A * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_battery_seq(p2pmg_ctx* c, int agents, int steps, const double* bal, double* out_bal, double* soc_hist,
+                      double* soc, const double* cap, double smin, double smax, double eff) {
+  if (!c || agents < 0 || steps < 0 || !bal || !out_bal || !soc_hist || !soc || !cap) return P2PMG_E_INVALID;
+  const size_t n = (size_t)agents * steps;
+  double* d = nullptr;
+  HIP_TRY(c, dmalloc(&d, 3 * n + 2 * (size_t)agents + 1));
+  double *db = d, *dob = d + n, *dsh = d + 2 * n, *ds = d + 3 * n, *dc = d + 3 * n + agents;
+  hipError_t e = hipMemcpyAsync(db, bal, n * 8, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(ds, soc, (size_t)agents * 8, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dc, cap, (size_t)agents * 8, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess)
+    e = p2pmg::launch_battery_seq(agents, steps, db, dob, dsh, ds, dc, smin, smax, std::sqrt(eff), c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_bal, dob, n * 8, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(soc_hist, dsh, n * 8, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(soc, ds, (size_t)agents * 8, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(d);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("battery_seq: ") + hipGetErrorString(e));
+  return P2PMG_OK;
+}
+
+int p2pmg_apply_q_delta(p2pmg_ctx* c) {
+  if (!c) return P2PMG_E_INVALID;
+  if (!c->qdelta) return fail(c, P2PMG_E_STATE, "apply_q_delta: context has no shared table");
+  HIP_TRY(c, p2pmg::launch_apply_delta(c->q, c->qdelta, c->n_states * kQPad, c->cfg.q_dtype, c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_get_q_delta(p2pmg_ctx* c, int64_t* host) {
+  if (!c || !host) return P2PMG_E_INVALID;
+  if (!c->qdelta) return fail(c, P2PMG_E_STATE, "get_q_delta: context has no shared table");
+  const int na = c->cfg.n_actions;
+  std::vector<long long> h(c->n_states * kQPad);
+  HIP_TRY(c, hipMemcpyAsync(h.data(), c->qdelta, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (size_t r = 0; r < c->n_states; ++r)
+    for (int k = 0; k < na; ++k) host[r * na + k] = h[r * kQPad + k];
+  return P2PMG_OK;
+}
+
+int p2pmg_comm_unique_id(uint8_t id[128]) {
+  if (!id) return P2PMG_E_INVALID;
+  Rccl* r = rccl();
+  if (!r) return P2PMG_E_UNSUPPORTED;
+  return r->getUniqueId(id) == 0 ? P2PMG_OK : P2PMG_E_HIP;
+}
+
+int p2pmg_comm_init(p2pmg_ctx* c, const uint8_t id[128], int rank, int nranks) {
+  if (!c || !id || rank < 0 || nranks <= 0 || rank >= nranks) return P2PMG_E_INVALID;
+  Rccl* r = rccl();
+  if (!r) return fail(c, P2PMG_E_UNSUPPORTED, "RCCL (librccl.so) not found");
+  HIP_TRY(c, hipSetDevice(c->device));
+  Id128 uid;
+  std::memcpy(uid.b, id, 128);
+  void* comm = nullptr;
+  const int rc = r->commInitRank(&comm, nranks, uid, rank);
+  if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclCommInitRank: ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
+  c->comm = comm;
+  return P2PMG_OK;
+}
+
+int p2pmg_allreduce_q_delta(p2pmg_ctx* c) {
+  if (!c) return P2PMG_E_INVALID;
+  if (!c->qdelta) return fail(c, P2PMG_E_STATE, "allreduce_q_delta: context has no shared table");
+  if (!c->comm) return fail(c, P2PMG_E_STATE, "allreduce_q_delta: p2pmg_comm_init first");
+  Rccl* r = rccl();
+  // ncclInt64 = 4, ncclSum = 0 (rccl.h)
+  const int rc = r->allReduce(c->qdelta, c->qdelta, c->n_states * kQPad, 4, 0, c->comm, c->stream);
+  if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclAllReduce: ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
+  return P2PMG_OK;
+}
+
+int p2pmg_comm_destroy(p2pmg_ctx* c) {
+  if (!c) return P2PMG_E_INVALID;
+  if (c->comm && rccl()) rccl()->commDestroy(c->comm);
+  c->comm = nullptr;
   return P2PMG_OK;
 }
 

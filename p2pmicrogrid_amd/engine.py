@@ -41,13 +41,14 @@ class DeviceCommunityBatch:
     """Device-resident batch of S communities.  All compute runs in libp2pmg.so."""
 
     def __init__(self, n_scenarios: int, n_agents: int, rounds: int, horizon: int, q_dtype: str = "f64",
-                 device: int = 0, seed: int = 42, scenario_offset: int = 0, **overrides):
+                 device: int = 0, seed: int = 42, scenario_offset: int = 0, shared_q: bool = False, **overrides):
         self.L = _lib.lib()
         cfg = _lib.default_config()
         cfg.n_scenarios, cfg.n_agents, cfg.rounds, cfg.horizon = n_scenarios, n_agents, rounds, horizon
         cfg.q_dtype = _lib.Q_F64 if q_dtype == "f64" else _lib.Q_F32
         cfg.seed = seed
         cfg.scenario_offset = scenario_offset
+        cfg.shared_q = int(bool(shared_q))
         for k, v in overrides.items():
             setattr(cfg, k, v)
         self.cfg = cfg
@@ -57,6 +58,8 @@ class DeviceCommunityBatch:
         self.device = device
         self.seed = seed
         self.scenario_offset = scenario_offset
+        self.shared_q = bool(shared_q)
+        self.n_tables = 1 if shared_q else self.A
         self.n_states = cfg.n_time_states * cfg.n_temp_states * cfg.n_balance_states * cfg.n_p2p_states
         self.q_shape = (cfg.n_time_states, cfg.n_temp_states, cfg.n_balance_states, cfg.n_p2p_states,
                         cfg.n_actions)
@@ -138,7 +141,7 @@ class DeviceCommunityBatch:
         self._chk(self.L.p2pmg_zero_q(self._ctx), "zero_q")
 
     def get_q(self, first: int = 0, count: Optional[int] = None, dtype=np.float64):
-        count = self.A - first if count is None else count
+        count = self.n_tables - first if count is None else count
         out = np.empty((count, *self.q_shape), dtype=dtype)
         code = _lib.Q_F64 if np.dtype(dtype) == np.float64 else _lib.Q_F32
         self._chk(self.L.p2pmg_get_q(self._ctx, first, count, out.ctypes.data, code), "get_q")
@@ -150,6 +153,59 @@ class DeviceCommunityBatch:
         t = np.ascontiguousarray(t.astype(dtype, copy=False).reshape(-1, self.n_states * self.q_shape[-1]))
         code = _lib.Q_F64 if dtype == np.float64 else _lib.Q_F32
         self._chk(self.L.p2pmg_set_q(self._ctx, first, t.shape[0], t.ctypes.data, code), "set_q")
+
+    # ----------------------------------------------------------------- heterogeneous agents / storage
+    def set_hp_levels(self, levels):
+        """Per-agent heat-pump power of actions 0..2 in W, [S, N, 3] (0 for agents without one)."""
+        lv = np.ascontiguousarray(np.asarray(levels, dtype=F32).reshape(self.A, 3))
+        self._chk(self.L.p2pmg_set_hp_levels(self._ctx, lv), "set_hp_levels")
+
+    def set_battery(self, capacity=None, min_soc=0.1, max_soc=0.9, efficiency=0.9, soc0=None):
+        """Battery per agent (capacity [S, N] in J, 0 = none); None disables storage."""
+        if capacity is None:
+            self._chk(self.L.p2pmg_set_battery(self._ctx, None, 0.1, 0.9, 1.0, None), "set_battery")
+            return
+        def per_agent(x):
+            x = np.asarray(x, np.float64)
+            return np.ascontiguousarray(x.reshape(self.A) if x.size == self.A else np.broadcast_to(x, (self.A,)))
+        cap = per_agent(capacity)
+        s0 = None if soc0 is None else per_agent(soc0)
+        self._chk(self.L.p2pmg_set_battery(self._ctx, cap.ctypes.data, float(min_soc), float(max_soc),
+                                           float(efficiency), None if s0 is None else s0.ctypes.data), "set_battery")
+
+    def get_soc(self):
+        out = np.empty(self.A, np.float64)
+        self._chk(self.L.p2pmg_get_soc(self._ctx, out.ctypes.data), "get_soc")
+        return out.reshape(self.S, self.N)
+
+    def battery_seq(self, balance, soc, capacity, min_soc=0.1, max_soc=0.9, efficiency=0.9):
+        """Battery rule (agent.py:138-153) over per-agent sequences [agents, steps] on the device."""
+        b = np.ascontiguousarray(np.atleast_2d(np.asarray(balance, np.float64)))
+        ag, st = b.shape
+        ob = np.empty_like(b)
+        sh = np.empty_like(b)
+        s_ = np.ascontiguousarray(np.broadcast_to(np.asarray(soc, np.float64), (ag,))).copy()
+        cap = np.ascontiguousarray(np.broadcast_to(np.asarray(capacity, np.float64), (ag,)))
+        self._chk(self.L.p2pmg_battery_seq(self._ctx, ag, st, b.ctypes.data, ob.ctypes.data, sh.ctypes.data,
+                                           s_.ctypes.data, cap.ctypes.data, float(min_soc), float(max_soc),
+                                           float(efficiency)), "battery_seq")
+        return ob, sh, s_
+
+    # ----------------------------------------------------------------- shared policy table
+    def apply_q_delta(self):
+        self._chk(self.L.p2pmg_apply_q_delta(self._ctx), "apply_q_delta")
+
+    def get_q_delta(self):
+        out = np.empty((self.n_states, self.q_shape[-1]), np.int64)
+        self._chk(self.L.p2pmg_get_q_delta(self._ctx, out.ctypes.data), "get_q_delta")
+        return out.reshape(self.q_shape)
+
+    def comm_init(self, unique_id: bytes, rank: int, nranks: int):
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._chk(self.L.p2pmg_comm_init(self._ctx, buf, rank, nranks), "comm_init")
+
+    def allreduce_q_delta(self):
+        self._chk(self.L.p2pmg_allreduce_q_delta(self._ctx), "allreduce_q_delta")
 
     # ----------------------------------------------------------------- the hot path
     def run_episode(self, mode: str = "train", rng: str = "replay", episode: int = 0, epsilon: float = 0.81,
@@ -238,6 +294,13 @@ def _q_calls(eng: "DeviceCommunityBatch", agents, s_obs, codes, rewards=None, ns
 
 
 DeviceCommunityBatch.q_calls = _q_calls
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId through libp2pmg (RCCL loaded at run time); rank 0 shares it."""
+    buf = (C.c_uint8 * 128)()
+    _lib.check(_lib.lib().p2pmg_comm_unique_id(buf), what="comm_unique_id")
+    return bytes(buf)
 
 
 def unpack_index(packed: np.ndarray) -> np.ndarray:

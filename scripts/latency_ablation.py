@@ -33,8 +33,8 @@ print(json.dumps(res))
 ''' % ROOT
 
 out = {}
-for name, lib in (("main", ""), ("noq", "build/libp2pmg_noq.so"), ("nodiv", "build/libp2pmg_nodiv.so"),
-                  ("noenv", "build/libp2pmg_noenv.so"), ("compute", "build/libp2pmg_compute.so")):
+for name, lib in (("main", ""), ("noq", "build/libp2pmg_noq.so"), 
+                  ("compute", "build/libp2pmg_compute.so")):
     env = dict(os.environ)
     if lib:
         env["P2PMG_LIB"] = os.path.join(ROOT, lib)

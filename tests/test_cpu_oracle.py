@@ -139,10 +139,13 @@ def test_reference_replay_codes_consumption_order():
     assert np.array_equal(codes.ravel(), np.array(want, np.uint8))
 
 
-def test_battery_fixture_is_consistent():
-    """The battery fixture (storage.py:36-76 + agent.py:138-153 rule) keeps SoC in bounds."""
+def test_battery_rule_matches_reference_storage():
+    """oracle.battery_rule vs the reference's BatteryStorage driven by the agent.py:138-153 rule."""
+    from oracle.restatement import battery_rule
     d = load_golden("battery")
+    soc = np.array(float(d["soc0"]))
+    for k, b in enumerate(d["bal"]):
+        ob, soc = battery_rule(np.array(b), soc, float(d["capacity"]), float(d["min_soc"]), float(d["max_soc"]),
+                               np.sqrt(float(d["efficiency"])))
+        assert ob == d["out_bal"][k] and soc == d["soc"][k], k
     assert np.all(d["soc"] >= 0.1 - 1e-12) and np.all(d["soc"] <= 0.9 + 1e-12)
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore")
-        assert np.isfinite(d["out_bal"]).all()

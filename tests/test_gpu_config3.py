@@ -1,0 +1,98 @@
+"""Configs 3-4 rows on the device vs the oracle: shared policy table with int64 fixed-point TD
+deltas (build-defined), battery storage (storage.py / agent.py:138-153),
+N = 16 agents, heterogeneous heat pumps and batteries, RCCL exchange of the deltas."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle.restatement import OracleBatch
+
+pytestmark = pytest.mark.gpu
+REC = ["reward", "cost", "grid", "p2p", "t_in", "action", "index"]
+
+
+def test_battery_primitive_matches_reference_storage():
+    from p2pmicrogrid_amd.engine import DeviceCommunityBatch
+    d = load_golden("battery")
+    eng = DeviceCommunityBatch(1, 1, 0, 1)
+    ob, sh, soc = eng.battery_seq(d["bal"][None], float(d["soc0"]), float(d["capacity"]), float(d["min_soc"]),
+                                  float(d["max_soc"]), float(d["efficiency"]))
+    assert np.array_equal(ob[0], d["out_bal"]) and np.array_equal(sh[0], d["soc"])
+
+
+def _setup(S, N, R, T, q_dtype, shared, battery, hetero, seed=9):
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    from p2pmicrogrid_amd.engine import DeviceCommunityBatch
+    inp = scenario_batch(S, N, T, seed=seed)
+    rs = np.random.RandomState(seed)
+    lv = np.broadcast_to(np.array([0.0, 1500.0, 3000.0], np.float32), (S, N, 3)).copy()
+    cap = np.full((S, N), 10 * 3.6e6) if battery else None
+    if hetero:  # config 4 mixes: some agents without heat pump, some without battery, other HP sizes
+        lv[rs.rand(S, N) < 0.25] = 0.0
+        big = rs.rand(S, N) < 0.3
+        lv[big] = np.array([0.0, 2500.0, 5000.0], np.float32)
+        if battery:
+            cap[rs.rand(S, N) < 0.4] = 0.0
+    ob = OracleBatch(S=S, N=N, R=R, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in, env_time=inp.time[None],
+                     env_tout=inp.t_out, q_dtype=q_dtype, shared_q=shared, hp_levels=lv, battery_capacity=cap)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, shared_q=shared)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    eng.set_hp_levels(lv)
+    if battery:
+        eng.set_battery(cap, 0.1, 0.9, 0.9)
+    return eng, ob
+
+
+def _cmp(out, rec, tag):
+    from p2pmicrogrid_amd.engine import unpack_index
+    for k in ("reward", "cost", "grid", "p2p", "t_in"):
+        assert np.array_equal(rec[k], out[k]), (tag, k)
+    assert np.array_equal(rec["action"], out["action"].astype(np.uint8)), tag
+    assert np.array_equal(unpack_index(rec["index"]), out["idx"]), tag
+
+
+@pytest.mark.parametrize("N,R,T,q_dtype,shared,battery,hetero", [
+    (16, 1, 24, "f32", True, True, False),     # config 3 shape
+    (16, 1, 24, "f64", True, False, False),
+    (2, 1, 96, "f64", True, True, False),
+    (4, 2, 32, "f64", False, True, True),      # config 4 shape: per-agent tables, mixed assets
+    (16, 1, 16, "f32", False, True, True),
+    (2, 1, 96, "f64", False, False, True),
+])
+def test_shared_battery_hetero_match_oracle(N, R, T, q_dtype, shared, battery, hetero):
+    S = 24
+    eng, ob = _setup(S, N, R, T, q_dtype, shared, battery, hetero)
+    for e in range(3):
+        eng.run_episode("train", "philox", episode=e, epsilon=0.6, record=REC)
+        out = ob.run_episode("train", rng="philox", episode=e, eps=0.6)
+        _cmp(out, eng.get_records(REC), (N, shared, battery, hetero, e))
+        if battery:
+            assert np.array_equal(eng.get_soc(), ob.soc)
+        if shared:
+            assert np.array_equal(eng.get_q_delta().reshape(-1, 3), ob.q_delta)
+            eng.apply_q_delta()
+            ob.apply_q_delta()
+            assert not eng.get_q_delta().any()
+        dt = np.float64 if q_dtype == "f64" else np.float32
+        assert np.array_equal(eng.get_q(dtype=dt).reshape(ob.q.shape), ob.q)
+    eng.run_episode("greedy", record=REC)
+    _cmp(ob.run_episode("greedy"), eng.get_records(REC), "greedy")
+
+
+def test_rccl_allreduce_world1_is_identity():
+    from p2pmicrogrid_amd.engine import comm_unique_id
+    eng, ob = _setup(16, 16, 1, 12, "f32", True, True, False)
+    eng.comm_init(comm_unique_id(), 0, 1)
+    eng.run_episode("train", "philox", episode=0, epsilon=0.5)
+    ob.run_episode("train", rng="philox", episode=0, eps=0.5)
+    before = eng.get_q_delta()
+    eng.allreduce_q_delta()
+    assert np.array_equal(eng.get_q_delta(), before)
+    assert np.array_equal(before.reshape(-1, 3), ob.q_delta)
+    eng.apply_q_delta()
+    ob.apply_q_delta()
+    assert np.array_equal(eng.get_q(dtype=np.float32).reshape(ob.q.shape), ob.q)
