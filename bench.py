@@ -12,6 +12,10 @@ synthetic profiles with the reference schema (the SQLite source is not available
 N GPUs: one process per GPU (torchrun), scenarios sharded with no data-path collective (each
 scenario's tables are private: "replicas only"); torch.distributed(gloo) carries only the
 barrier and the max-over-ranks time.  value = all ranks' agent-steps / max time (weak scaling).
+
+``--workload config3`` (BASELINE.json configs[2]): 1M scenarios x 16 agents with battery storage
+over 8 GPUs = 125,000 scenarios (2M agents) per GPU, ONE shared f32 Q-table whose int64
+fixed-point TD deltas are all-reduced over RCCL once per episode (the path's real exchange step).
 """
 from __future__ import annotations
 
@@ -35,6 +39,15 @@ def algorithmic_bytes_per_agent_step(R: int, q_bytes: int, outputs: int = 2) -> 
     next-state max, Q[s,a] read+write) + 4 * outputs (reward, cost).  The persistent variant keeps
     T_in/T_m in registers for the whole episode, so the 16 B of state traffic is dropped."""
     return 8 + q_bytes * (3 * (R + 1) + 3 + 2) + 4 * outputs
+
+
+def algorithmic_bytes_per_agent_step_shared(agents: int, q_bytes: int, battery: bool, outputs: int = 2) -> float:
+    """SURVEY.md §8(d), shared table: 8 (load_w, pv_w) + 4 * outputs + the table read once and its
+    int64 delta buffer read+written once per step, amortised over the agents of the step
+    (2 * |Q| * q_bytes + 2 * |Q| * 8) / agents.  T_in/T_m/SoC live in registers for the episode.
+    Per-agent gathers hit the same 1.9 MB table and are cache traffic, not HBM traffic."""
+    q_entries = 20 ** 4 * 3
+    return 8 + 4 * outputs + (2 * q_entries * q_bytes + 2 * q_entries * 8) / agents
 
 
 def epsilon_at(episode: int, eps0: float = 0.81, decay: float = 0.9, every: int = 50, floor: float = 0.1) -> float:
@@ -73,25 +86,39 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 96):
+BATTERY_J = 10.0 * 3.6e6  # 10 kWh per household battery (config 3; the reference fixes no size)
+
+WORKLOADS = {
+    # name: (scenarios per GPU, agents, rounds R, horizon, q dtype, shared table, battery)
+    "config2": (4096, 2, 1, 96, "f64", False, False),
+    "config3": (125000, 16, 1, 96, "f32", True, True),
+}
+
+
+def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 96, q_dtype: str = "f64",
+                 shared: bool = False, battery: bool = False):
     """The oracle (NumPy CPU restatement, oracle/restatement.py) on a bounded sample of the same
     workload, single-threaded, Philox exploration."""
     from oracle.restatement import OracleBatch
     from p2pmicrogrid_amd.dataset import scenario_batch
     inp = scenario_batch(S, N, T)
     ob = OracleBatch(S=S, N=N, R=R, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in,
-                     env_time=inp.time[None], env_tout=inp.t_out)
+                     env_time=inp.time[None], env_tout=inp.t_out, q_dtype=q_dtype, shared_q=shared,
+                     battery_capacity=np.full((S, N), BATTERY_J) if battery else None)
     ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
     t0 = time.perf_counter()
     eps_done = 0
     while True:
         ob.run_episode("train", rng="philox", episode=eps_done, eps=epsilon_at(eps_done))
+        if shared:
+            ob.apply_q_delta()
         eps_done += 1
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
+    what = "shared table + battery, " if shared else ""
     return {"value": S * N * T * eps_done / dt, "unit": "agent-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{S} scenarios x thesis community (N={N}, R={R}, T={T}), {eps_done} training episodes, "
+            "sample": f"{S} scenarios x N={N} (R={R}, T={T}, {what}{q_dtype} Q), {eps_done} training episodes, "
                       f"oracle/restatement.py vectorised NumPy, {dt:.1f} s"}
 
 
@@ -113,11 +140,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50, help="timed episodes")
     ap.add_argument("--warmup", type=int, default=5, help="untimed episodes")
-    ap.add_argument("--scenarios", type=int, default=4096, help="scenarios per GPU (configs[1]: 4096)")
-    ap.add_argument("--agents", type=int, default=2)
-    ap.add_argument("--rounds", type=int, default=1)
-    ap.add_argument("--horizon", type=int, default=96)
-    ap.add_argument("--q-dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS),
+                    help="config2 = BASELINE configs[1] (default); config3 = configs[2] per-GPU slice")
+    ap.add_argument("--scenarios", type=int, default=None, help="override scenarios per GPU")
+    ap.add_argument("--agents", type=int, default=None)
+    ap.add_argument("--rounds", type=int, default=None)
+    ap.add_argument("--horizon", type=int, default=None)
+    ap.add_argument("--q-dtype", default=None, choices=["f64", "f32"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -127,18 +156,34 @@ def main():
     from p2pmicrogrid_amd.dataset import scenario_batch
     from p2pmicrogrid_amd.engine import DeviceCommunityBatch
 
-    S, N, R, T = args.scenarios, args.agents, args.rounds, args.horizon
+    S, N, R, T, q_dtype, shared, battery = WORKLOADS[args.workload]
+    S = args.scenarios or S
+    N = args.agents or N
+    R = R if args.rounds is None else args.rounds
+    T = args.horizon or T
+    q_dtype = args.q_dtype or q_dtype
     first = rank * S
     inp = scenario_batch(S, N, T, first_scenario=first)
-    eng = DeviceCommunityBatch(S, N, R, T, q_dtype=args.q_dtype, device=local, scenario_offset=first)
+    eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=local, scenario_offset=first, shared_q=shared)
     eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
     eng.set_profiles(inp.load_w, inp.pv_w)
     eng.set_max_in(inp.max_in)
     eng.set_temperatures(inp.t_in0, inp.t_m0)
+    del inp
+    if battery:
+        eng.set_battery(BATTERY_J)
+    if shared and world > 1:  # RCCL communicator for the per-episode delta all-reduce (xGMI)
+        from p2pmicrogrid_amd.distributed import broadcast_bytes
+        from p2pmicrogrid_amd.engine import comm_unique_id
+        eng.comm_init(broadcast_bytes(comm_unique_id() if rank == 0 else None, world), rank, world)
     record = ("reward", "cost")
 
     def episode(e):
         eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record)
+        if shared:
+            if world > 1:
+                eng.allreduce_q_delta()
+            eng.apply_q_delta()
         eng.reset_temperatures_philox(e + 1, 0.3)  # agent.reset() at the end of train_episode
 
     for e in range(args.warmup):
@@ -159,12 +204,17 @@ def main():
 
     steps_per_episode = S * N * T
     value = world * steps_per_episode * args.steps / dt
-    q_bytes = 8 if args.q_dtype == "f64" else 4
-    bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
+    q_bytes = 8 if q_dtype == "f64" else 4
+    if shared:
+        bpa = algorithmic_bytes_per_agent_step_shared(S * N, q_bytes, battery, outputs=len(record))
+        workload = (f"configs[2]: {S} scenarios/GPU x {N} agents (R={R}, T={T}) with battery storage, one shared "
+                    f"{q_dtype} Q-table, int64 delta all-reduce per episode, Philox exploration, train episodes")
+    else:
+        bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
+        workload = (f"configs[1]: {S} scenarios/GPU x thesis community (N={N}, R={R}, T={T}), per-agent "
+                    f"{q_dtype} Q-tables, Philox exploration, train episodes")
     kernel_ms = float(np.mean(kms)) if len(kms) else float("nan")
     achieved = bpa * steps_per_episode / (kernel_ms * 1e-3) / 1e9
-    workload = (f"configs[1]: {S} scenarios/GPU x thesis community (N={N}, R={R}, T={T}), per-agent "
-                f"{args.q_dtype} Q-tables, Philox exploration, train episodes")
     traffic = load_traffic(args.traffic_json, workload)
     if rank == 0:
         out = {
@@ -178,16 +228,18 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 simulation, f64 Q-table" if args.q_dtype == "f64" else "f32",
+            "dtype": "f32 simulation, f64 Q-table" if q_dtype == "f64" else "f32",
             "data": "synthetic profiles with the reference dataset schema (seed 42)",
             "config": {"workload": workload, "scenarios_per_gpu": S, "agents_per_scenario": N,
-                       "rounds": R + 1, "horizon": T, "q_dtype": args.q_dtype,
+                       "rounds": R + 1, "horizon": T, "q_dtype": q_dtype, "shared_q": shared, "battery": battery,
                        "agent_steps_per_step": world * steps_per_episode,
-                       "parallelism": f"scenario-sharded x{world} (replicas, no data-path collective)"},
+                       "parallelism": (f"scenario-sharded x{world}, shared-table delta all-reduce (RCCL)" if shared
+                                       else f"scenario-sharded x{world} (replicas, no data-path collective)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
-                         "kernel": "episode_kernel<2,double>", "kernel_ms": kernel_ms,
+                         "kernel": f"episode_kernel<{N},{'double' if q_bytes == 8 else 'float'}>",
+                         "kernel_ms": kernel_ms,
                          "algorithmic_bytes_per_agent_step": bpa,
                          "algorithmic_bytes_per_launch": bpa * steps_per_episode,
                          "timed_launches": int(len(kms))},
@@ -196,7 +248,8 @@ def main():
         if traffic:
             out["roofline"]["traffic_source"] = traffic.get("source")
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, N=N, R=R, T=T)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, S=256 if N <= 4 else 64, N=N, R=R, T=T,
+                                               q_dtype=q_dtype, shared=shared, battery=battery)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

@@ -185,6 +185,7 @@ int p2pmg_battery_seq(p2pmg_ctx* ctx, int agents, int steps, const double* balan
 /* shared policy table (config.shared_q = 1) */
 int p2pmg_apply_q_delta(p2pmg_ctx* ctx);            /* Q += delta * 2^-40; delta = 0 */
 int p2pmg_get_q_delta(p2pmg_ctx* ctx, int64_t* host); /* [n_states][n_actions] fixed point */
+int p2pmg_set_q_delta(p2pmg_ctx* ctx, const int64_t* host); /* e.g. after a host-side (gloo) sum */
 
 /* multi-GPU exchange of the shared-table deltas over RCCL (xGMI), loaded at run time */
 int p2pmg_comm_unique_id(uint8_t id[128]);

@@ -81,3 +81,26 @@ def t0_draws(seed: int, episode: int, agents, setpoint: float = 21.0, sigma: flo
     z0 = rad * np.cos(ang)
     z1 = rad * np.sin(ang)
     return (setpoint + sigma * z0).astype(np.float32), (setpoint + sigma * z1).astype(np.float32)
+
+
+TAG_SAMPLE = 0x5EED0100  # + j, j < 32: replay-buffer sample draws (DQN)
+
+
+def sample_draws(seed: int, episode: int, agents, t: int, count, k: int = 32):
+    """Build-defined replay-buffer sampling in Philox mode (DQN, rl.py:226-241 semantics:
+    k distinct indices of [0, count), 0 = oldest).  Floyd's algorithm: for j = 0..k-1,
+    m = count - k + j, r = (x0_j * (m + 1)) >> 32 with x0_j the first word of the Philox block
+    ctr = (t, episode, agent, TAG_SAMPLE + j); take r unless already taken, else m.
+    Returns int64 [len(agents), k] in draw order."""
+    agents = np.asarray(agents, dtype=np.uint64).ravel()
+    count = np.broadcast_to(np.asarray(count, dtype=np.int64), agents.shape)
+    k0 = seed & 0xFFFFFFFF
+    k1 = (seed >> 32) & 0xFFFFFFFF
+    out = np.zeros((len(agents), k), dtype=np.int64)
+    for j in range(k):
+        x0, _, _, _ = philox4x32_10(t, episode, agents, TAG_SAMPLE + j, k0, k1)
+        m = count - k + j
+        r = ((x0 * (m + 1).astype(np.uint64)) >> np.uint64(32)).astype(np.int64)
+        taken = (out[:, :j] == r[:, None]).any(axis=1) if j else np.zeros(len(agents), bool)
+        out[:, j] = np.where(taken, m, r)
+    return out

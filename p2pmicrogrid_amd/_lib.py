@@ -29,7 +29,7 @@ EXPORTS = [
     "p2pmg_get_record", "p2pmg_get_episode_reward", "p2pmg_last_kernel_ms", "p2pmg_rc_step",
     "p2pmg_state_indices", "p2pmg_replay_decode", "p2pmg_device_count", "p2pmg_kernel_times",
     "p2pmg_reset_kernel_times", "p2pmg_q_calls", "p2pmg_set_hp_levels", "p2pmg_set_battery", "p2pmg_get_soc",
-    "p2pmg_battery_seq", "p2pmg_apply_q_delta", "p2pmg_get_q_delta", "p2pmg_comm_unique_id", "p2pmg_comm_init",
+    "p2pmg_battery_seq", "p2pmg_apply_q_delta", "p2pmg_get_q_delta", "p2pmg_set_q_delta", "p2pmg_comm_unique_id", "p2pmg_comm_init",
     "p2pmg_allreduce_q_delta", "p2pmg_comm_destroy",
 ]
 
@@ -104,6 +104,7 @@ def _declare(lib):
         "p2pmg_battery_seq": ([vp, i32, i32, vp, vp, vp, vp, vp, C.c_double, C.c_double, C.c_double], i32),
         "p2pmg_apply_q_delta": ([vp], i32),
         "p2pmg_get_q_delta": ([vp, vp], i32),
+        "p2pmg_set_q_delta": ([vp, vp], i32),
         "p2pmg_comm_unique_id": ([vp], i32),
         "p2pmg_comm_init": ([vp, vp, i32, i32], i32),
         "p2pmg_allreduce_q_delta": ([vp], i32),

@@ -12,6 +12,9 @@ constexpr int kWave = 64;      // one wave per workgroup
 constexpr int kMaxAgents = 16; // compiled-in agents per scenario
 constexpr int kMaxRounds1 = 8; // R + 1 <= 8 (two code words)
 constexpr double kDeltaScale = 1099511627776.0;  // 2^40: shared-table TD deltas in int64 fixed point
+// shared-table delta replicas: workgroup b accumulates into copy (b % 8), i.e. its own XCD\'s copy
+// (blocks are dealt round-robin over the 8 XCDs); the copies are folded before use
+constexpr int kDeltaCopies = 8;
 
 // Everything the episode kernel needs, passed by value in the kernarg segment.
 struct EpisodeParams {
@@ -39,7 +42,7 @@ struct EpisodeParams {
   // shared policy (config 3): every agent reads one frozen table; TD deltas accumulate in
   // int64 fixed point (2^-40) with device atomics, applied at episode end (p2pmg_apply_q_delta)
   int shared_q;
-  long long* qdelta;         // [n_states][kQPad] int64
+  long long* qdelta;         // [kDeltaCopies][n_states][kQPad] int64 (one replica per XCD)
   // battery (agent.py:138-153 rule, storage.py:36-76 bookkeeping), f64 like the reference
   int battery;
   double* soc;               // [A] in/out
@@ -60,6 +63,7 @@ struct RcParams {
 
 hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream);
 hipError_t launch_apply_delta(void* q, long long* qdelta, size_t n, int q_dtype, hipStream_t stream);
+hipError_t launch_fold_delta(long long* qdelta, size_t n, hipStream_t stream);
 hipError_t launch_battery_seq(int agents, int steps, const double* bal, double* out_bal, double* soc_hist,
                               double* soc, const double* cap, double smin, double smax, double sqrt_eff,
                               hipStream_t stream);

@@ -408,6 +408,31 @@ __device__ __forceinline__ float hp_of(const float4& lv, int act) { return sel3(
 //     the next-state row, is known as soon as the previous step's final action is: both are
 //     issued right after that action, before the previous step's market/reward/TD work;
 //   * a TD store that hits one of those prefetched rows patches the register copy.
+// Shared-table variant: each workgroup sums its agents' int64 TD deltas for the whole episode in
+// an LDS hash table (linear probing, ds_cmpst + ds_add_u64) and flushes one global atomic per
+// occupied slot at the end.  All agents of a step share the time bin, so the episode's deltas
+// hit only a few thousand entries: without the table, millions of same-address global atomics
+// per step serialise.  Exact integer sums, so the grouping never changes the result.
+constexpr int kSqWaves = 4;          // waves per workgroup
+constexpr int kSqSlotBits = 11;      // 2048 slots: 8 KB keys + 16 KB sums
+constexpr int kSqSlots = 1 << kSqSlotBits;
+constexpr uint32_t kSqEmpty = 0xFFFFFFFFu;
+
+__device__ __forceinline__ void lds_add_by_key(uint32_t* hk, unsigned long long* hv, uint32_t key, long long v,
+                                               unsigned long long* gbase) {
+  if (v == 0) return;
+  uint32_t h = (key * 2654435761u) >> (32 - kSqSlotBits);
+  for (int probe = 0; probe < 32; ++probe) {
+    const uint32_t prev = atomicCAS(hk + h, kSqEmpty, key);
+    if (prev == kSqEmpty || prev == key) {
+      atomicAdd(hv + h, (unsigned long long)v);
+      return;
+    }
+    h = (h + 1) & (kSqSlots - 1);
+  }
+  atomicAdd(gbase + key, (unsigned long long)v);  // crowded table: straight to the global replica
+}
+
 template <typename QT>
 __device__ __forceinline__ Row4<QT> gather_row(const QT* p) {
 #if P2PMG_ABLATE == 1 || P2PMG_ABLATE == 4
@@ -417,17 +442,25 @@ __device__ __forceinline__ Row4<QT> gather_row(const QT* p) {
   return load_row(p);
 #endif
 }
-template <int N, typename QT, bool B20>
-__global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
+template <int N, typename QT, bool B20, bool SQ>
+__global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(const EpisodeParams p) {
   constexpr int G = pow2ceil(N);
   constexpr int SPW = kWave / G;
-  __shared__ float shP[G > 8 ? SPW * N * N : 1];
-  __shared__ float shR[G > 8 ? SPW * N : 1];
+  constexpr int WPB = SQ ? kSqWaves : 1;  // waves per workgroup
+  constexpr int PW = G > 8 ? SPW * N * N : 1;
+  constexpr int RW = G > 8 ? SPW * N : 1;
+  __shared__ float shPall[WPB * PW];
+  __shared__ float shRall[WPB * RW];
+  __shared__ uint32_t hkey[SQ ? kSqSlots : 1];
+  __shared__ unsigned long long hval[SQ ? kSqSlots : 1];
 
-  const int lane = threadIdx.x;
+  const int wv = SQ ? (int)(threadIdx.x / kWave) : 0;
+  const int lane = SQ ? (int)(threadIdx.x % kWave) : (int)threadIdx.x;
+  float* const shP = shPall + wv * PW;  // this wave's exchange tile
+  float* const shR = shRall + wv * RW;
   const int sl = lane / G;
   const int i = lane % G;
-  const int s = blockIdx.x * SPW + sl;
+  const int s = (blockIdx.x * WPB + wv) * SPW + sl;
   const bool in_group = i < N;
   const bool active = in_group && (s < p.S);
   const int a = active ? s * N + i : 0;
@@ -443,8 +476,17 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
   const Dims<B20> D{k.nt, k.nT, k.nb, k.np};
 
   const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
-  const bool shared = p.shared_q != 0;
+  constexpr bool shared = SQ;
   QT* __restrict__ q = reinterpret_cast<QT*>(p.q) + (shared ? (size_t)0 : (size_t)a * n_states * kQPad);
+  unsigned long long* const dbase = reinterpret_cast<unsigned long long*>(p.qdelta) +
+      (shared ? (size_t)(blockIdx.x % kDeltaCopies) * n_states * kQPad : (size_t)0);
+  if constexpr (SQ) {
+    for (int k2 = threadIdx.x; k2 < kSqSlots; k2 += WPB * kWave) {
+      hkey[k2] = kSqEmpty;
+      hval[k2] = 0;
+    }
+    __syncthreads();
+  }
   const float mi = active ? p.max_in[a] : 1.0f;
   const float4 lv = p.hp_lv[a];  // heat-pump power of actions 0..2 for this agent
   const bool bat = p.battery != 0;
@@ -603,21 +645,24 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
     pen = pen > 0.0f ? pen + 1.0f : 0.0f;
     const float rw = -(cost + k.penw * pen);
 
-    if (train && active) {
+    if (train && active && !shared) {
       // QAgent.train agent.py:293-298 -> QActor.train rl.py:119-129
       const uint32_t srow = st.strip + ip;
       const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
-      if (shared) {
-        // frozen shared table: delta = alpha * ((r + gamma * max Q[ns]) - Q[s, a]) in f64, summed in
-        // int64 fixed point (order-independent, so every launch and every rank sums identically)
-        const double d = k.alpha * (((double)rw + k.gamma * (double)max3(rowN)) - (double)qsa);
-        atomicAdd(reinterpret_cast<unsigned long long*>(p.qdelta) + (size_t)srow * kQPad + act,
-                  (unsigned long long)__double2ll_rn(d * kDeltaScale));
-      } else {
-        const QT qnew = td_update(qsa, rw, max3(rowN), k.alpha, k.gamma);
-        q[srow * kQPad + act] = qnew;
-        pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
-      }
+      const QT qnew = td_update(qsa, rw, max3(rowN), k.alpha, k.gamma);
+      q[srow * kQPad + act] = qnew;
+      pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
+    }
+    if (shared && train && active) {
+      // frozen shared table: delta = alpha * ((r + gamma * max Q[ns]) - Q[s, a]) in f64, summed in
+      // int64 fixed point (order-independent, so every launch and every rank sums identically)
+      const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
+      const double d = k.alpha * (((double)rw + k.gamma * (double)max3(rowN)) - (double)qsa);
+      const long long v = __double2ll_rn(d * kDeltaScale);
+#if P2PMG_ABLATE == 5
+      if (v == 12345)  // timing-only: drop the accumulation (never true in practice)
+#endif
+      lds_add_by_key(hkey, hval, (st.strip + (uint32_t)ip) * kQPad + (uint32_t)act, v, dbase);
     }
     if (active && (rec & 31u)) {
       if (rec & 1u) rec_reward[tA] = rw;
@@ -651,6 +696,16 @@ __global__ __launch_bounds__(kWave) void episode_kernel(const EpisodeParams p) {
     if (bat) p.soc[a] = soc;
     if (i == 0) p.ep_reward[s] = ep_sum;
   }
+  if constexpr (SQ) {
+    if (train) {  // block-uniform: flush the episode's sums into this XCD's replica
+      __syncthreads();
+      for (int k2 = threadIdx.x; k2 < kSqSlots; k2 += WPB * kWave) {
+        const uint32_t key = hkey[k2];
+        const long long x = (long long)hval[k2];
+        if (key != kSqEmpty && x != 0) atomicAdd(dbase + key, (unsigned long long)x);
+      }
+    }
+  }
 }
 
 // Q += delta * 2^-40 (f64), delta = 0: the end-of-episode update of the shared table, after the
@@ -664,6 +719,22 @@ __global__ void apply_delta_kernel(QT* __restrict__ q, long long* __restrict__ d
     q[k] = (QT)((double)q[k] + (double)x * (1.0 / kDeltaScale));
     d[k] = 0;
   }
+}
+
+// sum the per-XCD delta replicas into copy 0 (and clear the others)
+__global__ void fold_delta_kernel(long long* __restrict__ d, size_t n) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  long long x = d[k];
+#pragma unroll
+  for (int c = 1; c < kDeltaCopies; ++c) {
+    const long long y = d[(size_t)c * n + k];
+    if (y != 0) {
+      x += y;
+      d[(size_t)c * n + k] = 0;
+    }
+  }
+  d[k] = x;
 }
 
 // battery rule over per-agent sequences (unit parity with storage.py / agent.py:138-153)
@@ -713,14 +784,24 @@ __global__ void pack_codes_kernel(int T, int R1, int A, const uint8_t* __restric
   }
 }
 
+template <int N, typename QT, bool SQ>
+void launch_nq(const EpisodeParams& p, hipStream_t st) {
+  constexpr int SPW = kWave / pow2ceil(N);
+  constexpr int WPB = SQ ? kSqWaves : 1;
+  const int waves = (p.S + SPW - 1) / SPW;
+  const int blocks = (waves + WPB - 1) / WPB;
+  if (p.nt == 20 && p.nT == 20 && p.nb == 20 && p.np == 20)
+    hipLaunchKernelGGL((episode_kernel<N, QT, true, SQ>), dim3(blocks), dim3(kWave * WPB), 0, st, p);
+  else
+    hipLaunchKernelGGL((episode_kernel<N, QT, false, SQ>), dim3(blocks), dim3(kWave * WPB), 0, st, p);
+}
+
 template <int N, typename QT>
 hipError_t launch_n(const EpisodeParams& p, hipStream_t st) {
-  constexpr int SPW = kWave / pow2ceil(N);
-  const int blocks = (p.S + SPW - 1) / SPW;
-  if (p.nt == 20 && p.nT == 20 && p.nb == 20 && p.np == 20)
-    hipLaunchKernelGGL((episode_kernel<N, QT, true>), dim3(blocks), dim3(kWave), 0, st, p);
+  if (p.shared_q)
+    launch_nq<N, QT, true>(p, st);
   else
-    hipLaunchKernelGGL((episode_kernel<N, QT, false>), dim3(blocks), dim3(kWave), 0, st, p);
+    launch_nq<N, QT, false>(p, st);
   return hipGetLastError();
 }
 
@@ -836,6 +917,11 @@ hipError_t launch_pack_codes(int T, int R1, int A, const uint8_t* in, uint32_t* 
   const size_t n = (size_t)T * A;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(pack_codes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, T, R1, A, in, words);
+  return hipGetLastError();
+}
+
+hipError_t launch_fold_delta(long long* qdelta, size_t n, hipStream_t stream) {
+  hipLaunchKernelGGL(fold_delta_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, qdelta, n);
   return hipGetLastError();
 }
 

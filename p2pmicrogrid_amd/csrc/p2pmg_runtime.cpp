@@ -50,7 +50,7 @@ struct p2pmg_ctx {
   double* bat_cap = nullptr;   // [A]
   bool battery = false;
   double bat_min = 0.1, bat_max = 0.9, bat_sqrt_eff = 1.0;
-  long long* qdelta = nullptr; // shared table deltas [n_states][4]
+  long long* qdelta = nullptr; // shared table deltas [kDeltaCopies][n_states][4]
   void* comm = nullptr;        // ncclComm_t
   bool have_env = false, have_prof = false, have_params = false, have_codes = false;
   std::string err;
@@ -232,8 +232,9 @@ int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
   const size_t qbytes = n_tables * c->n_states * kQPad * c->q_elem;
   if (hipMalloc(&c->q, qbytes) != hipSuccess) return bail(P2PMG_E_NOMEM);
   if (cfg->shared_q) {
-    if (dmalloc(&c->qdelta, c->n_states * kQPad) != hipSuccess) return bail(P2PMG_E_NOMEM);
-    if (hipMemsetAsync(c->qdelta, 0, c->n_states * kQPad * 8, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
+    if (dmalloc(&c->qdelta, p2pmg::kDeltaCopies * c->n_states * kQPad) != hipSuccess) return bail(P2PMG_E_NOMEM);
+    if (hipMemsetAsync(c->qdelta, 0, p2pmg::kDeltaCopies * c->n_states * kQPad * 8, c->stream) != hipSuccess)
+      return bail(P2PMG_E_HIP);
   }
   if (dmalloc(&c->hp_lv, A) != hipSuccess || dmalloc(&c->soc, A) != hipSuccess) return bail(P2PMG_E_NOMEM);
   {
@@ -408,7 +409,7 @@ int p2pmg_zero_q(p2pmg_ctx* c) {
   if (!c) return P2PMG_E_INVALID;
   const size_t n_tables = c->cfg.shared_q ? 1 : (size_t)c->A;
   HIP_TRY(c, hipMemsetAsync(c->q, 0, n_tables * c->n_states * kQPad * c->q_elem, c->stream));
-  if (c->qdelta) HIP_TRY(c, hipMemsetAsync(c->qdelta, 0, c->n_states * kQPad * 8, c->stream));
+  if (c->qdelta) HIP_TRY(c, hipMemsetAsync(c->qdelta, 0, p2pmg::kDeltaCopies * c->n_states * kQPad * 8, c->stream));
   return P2PMG_OK;
 }
 
@@ -724,6 +725,7 @@ int p2pmg_battery_seq(p2pmg_ctx* c, int agents, int steps, const double* bal, do
 int p2pmg_apply_q_delta(p2pmg_ctx* c) {
   if (!c) return P2PMG_E_INVALID;
   if (!c->qdelta) return fail(c, P2PMG_E_STATE, "apply_q_delta: context has no shared table");
+  HIP_TRY(c, p2pmg::launch_fold_delta(c->qdelta, c->n_states * kQPad, c->stream));
   HIP_TRY(c, p2pmg::launch_apply_delta(c->q, c->qdelta, c->n_states * kQPad, c->cfg.q_dtype, c->stream));
   return P2PMG_OK;
 }
@@ -733,10 +735,24 @@ int p2pmg_get_q_delta(p2pmg_ctx* c, int64_t* host) {
   if (!c->qdelta) return fail(c, P2PMG_E_STATE, "get_q_delta: context has no shared table");
   const int na = c->cfg.n_actions;
   std::vector<long long> h(c->n_states * kQPad);
+  HIP_TRY(c, p2pmg::launch_fold_delta(c->qdelta, c->n_states * kQPad, c->stream));
   HIP_TRY(c, hipMemcpyAsync(h.data(), c->qdelta, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   for (size_t r = 0; r < c->n_states; ++r)
     for (int k = 0; k < na; ++k) host[r * na + k] = h[r * kQPad + k];
+  return P2PMG_OK;
+}
+
+int p2pmg_set_q_delta(p2pmg_ctx* c, const int64_t* host) {
+  if (!c || !host) return P2PMG_E_INVALID;
+  if (!c->qdelta) return fail(c, P2PMG_E_STATE, "set_q_delta: context has no shared table");
+  const int na = c->cfg.n_actions;
+  std::vector<long long> h(c->n_states * kQPad, 0);
+  for (size_t r = 0; r < c->n_states; ++r)
+    for (int k = 0; k < na; ++k) h[r * kQPad + k] = host[r * na + k];
+  HIP_TRY(c, hipMemsetAsync(c->qdelta, 0, p2pmg::kDeltaCopies * h.size() * 8, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->qdelta, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return P2PMG_OK;
 }
 
@@ -767,6 +783,7 @@ int p2pmg_allreduce_q_delta(p2pmg_ctx* c) {
   if (!c->comm) return fail(c, P2PMG_E_STATE, "allreduce_q_delta: p2pmg_comm_init first");
   Rccl* r = rccl();
   // ncclInt64 = 4, ncclSum = 0 (rccl.h)
+  HIP_TRY(c, p2pmg::launch_fold_delta(c->qdelta, c->n_states * kQPad, c->stream));
   const int rc = r->allReduce(c->qdelta, c->qdelta, c->n_states * kQPad, 4, 0, c->comm, c->stream);
   if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclAllReduce: ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
   return P2PMG_OK;

@@ -6,6 +6,12 @@ every rank's tables are private: this is "replicas only" — the only collective
 end-of-episode reduction of the episode metrics (a few bytes, over torch.distributed).
 Philox counters use global agent ids and scenario data depend only on (seed, scenario), so
 any world size reproduces the single-GPU results scenario for scenario.
+
+With ONE shared policy table (config 3, ``shared_q=True``) there is a real exchange step: every
+rank accumulates its scenarios' TD deltas in int64 fixed point, the deltas are summed over the
+ranks once per episode (RCCL all-reduce on the device stream, or a host-side sum over the
+process group), and each rank applies the identical sum.  Integer addition is associative, so
+the table after each episode is bit-identical for every world size.
 """
 from __future__ import annotations
 
@@ -55,6 +61,26 @@ def all_reduce_sum(values: np.ndarray, world: int) -> np.ndarray:
     return t.numpy()
 
 
+def all_reduce_int64(values: np.ndarray, world: int) -> np.ndarray:
+    """Exact int64 sum over ranks (host fallback of the shared-table delta exchange)."""
+    if world == 1:
+        return np.asarray(values, dtype=np.int64)
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(values, dtype=np.int64))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.numpy()
+
+
+def broadcast_bytes(data: Optional[bytes], world: int, src: int = 0) -> bytes:
+    if world == 1:
+        return data
+    import torch.distributed as dist
+    box = [data]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]
+
+
 def all_gather_concat(values: np.ndarray, world: int) -> np.ndarray:
     """Concatenate per-rank 1-D arrays in rank order (ragged allowed)."""
     if world == 1:
@@ -68,34 +94,67 @@ def all_gather_concat(values: np.ndarray, world: int) -> np.ndarray:
 class ShardedTrainer:
     """Tabular training of S_total scenarios sharded over the ranks.
 
-    engine_factory(shard, S, N, R, T, q_dtype, device, seed) -> an object with the
-    DeviceCommunityBatch interface; the default is the HIP engine."""
+    engine_factory(shard, S, N, R, T, q_dtype, device, seed, shared_q) -> an object with the
+    DeviceCommunityBatch interface; the default is the HIP engine.
+
+    shared_q: one policy table for every agent of every scenario on every rank (config 3).
+    exchange: how the shared-table deltas are summed over ranks — "rccl" (device all-reduce over
+    xGMI, the production path), "host" (copy out, sum over the torch process group, copy back)
+    or "auto" (rccl when the process group is nccl/RCCL, host otherwise).
+    battery: kwargs for ``set_battery`` (scalars), enabling the storage rule."""
 
     def __init__(self, n_scenarios: int, n_agents: int = 2, rounds: int = 1, horizon: int = 96,
                  q_dtype: str = "f64", seed: int = 42, rank: int = 0, world: int = 1, device: int = 0,
-                 engine_factory: Optional[Callable] = None):
+                 engine_factory: Optional[Callable] = None, shared_q: bool = False, exchange: str = "auto",
+                 battery: Optional[dict] = None, homogeneous: bool = False):
         from .dataset import scenario_batch
         self.sh = shard(n_scenarios, rank, world)
         self.S_total, self.N, self.R, self.T = n_scenarios, n_agents, rounds, horizon
-        self.world = world
-        inp = scenario_batch(self.sh.count, n_agents, horizon, seed=seed, first_scenario=self.sh.first)
+        self.rank, self.world, self.shared_q = rank, world, bool(shared_q)
+        inp = scenario_batch(self.sh.count, n_agents, horizon, seed=seed, first_scenario=self.sh.first,
+                             homogeneous=homogeneous)
         if engine_factory is None:
             from .engine import DeviceCommunityBatch
 
-            def engine_factory(sh, S, N, R, T, q_dtype, device, seed):
+            def engine_factory(sh, S, N, R, T, q_dtype, device, seed, shared_q=False):
                 return DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=device, seed=seed,
-                                            scenario_offset=sh.first)
-        self.eng = engine_factory(self.sh, self.sh.count, n_agents, rounds, horizon, q_dtype, device, seed)
+                                            scenario_offset=sh.first, shared_q=shared_q)
+        self.eng = engine_factory(self.sh, self.sh.count, n_agents, rounds, horizon, q_dtype, device, seed,
+                                  shared_q=self.shared_q)
         self.eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
         self.eng.set_profiles(inp.load_w, inp.pv_w)
         self.eng.set_max_in(inp.max_in)
         self.eng.set_temperatures(inp.t_in0, inp.t_m0)
+        if battery is not None:
+            self.eng.set_battery(**battery)
+        self.exchange = None
+        if self.shared_q and world > 1:
+            if exchange == "auto":
+                import torch.distributed as dist
+                exchange = "rccl" if dist.is_initialized() and dist.get_backend() == "nccl" else "host"
+            if exchange not in ("rccl", "host"):
+                raise ValueError(f"exchange must be 'rccl', 'host' or 'auto', got {exchange!r}")
+            if exchange == "rccl":
+                from .engine import comm_unique_id
+                uid = broadcast_bytes(comm_unique_id() if rank == 0 else None, world)
+                self.eng.comm_init(uid, rank, world)
+            self.exchange = exchange
         self.episode = 0
+
+    def exchange_q_delta(self):
+        """Sum the shared-table deltas over the ranks and apply them (once per episode)."""
+        if self.exchange == "rccl":
+            self.eng.allreduce_q_delta()
+        elif self.exchange == "host":
+            self.eng.set_q_delta(all_reduce_int64(self.eng.get_q_delta(), self.world))
+        self.eng.apply_q_delta()
 
     def train_episode(self, epsilon: float, reset_sigma: float = 0.3) -> float:
         """One training episode on every shard; returns the global mean over scenarios of the
         episode reward (sum_t mean_i r, community.py:179)."""
         self.eng.run_episode("train", "philox", episode=self.episode, epsilon=epsilon)
+        if self.shared_q:
+            self.exchange_q_delta()
         local = self.eng.episode_reward().astype(np.float64)
         self.eng.reset_temperatures_philox(self.episode + 1, reset_sigma)
         self.episode += 1

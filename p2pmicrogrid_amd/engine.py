@@ -200,6 +200,10 @@ class DeviceCommunityBatch:
         self._chk(self.L.p2pmg_get_q_delta(self._ctx, out.ctypes.data), "get_q_delta")
         return out.reshape(self.q_shape)
 
+    def set_q_delta(self, delta):
+        d = np.ascontiguousarray(np.asarray(delta, np.int64).reshape(self.n_states, self.q_shape[-1]))
+        self._chk(self.L.p2pmg_set_q_delta(self._ctx, d.ctypes.data), "set_q_delta")
+
     def comm_init(self, unique_id: bytes, rank: int, nranks: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         self._chk(self.L.p2pmg_comm_init(self._ctx, buf, rank, nranks), "comm_init")

@@ -7,8 +7,10 @@ from oracle.restatement import OracleBatch
 
 
 class OracleEngine:
-    def __init__(self, sh, S, N, R, T, q_dtype, device, seed):
+    def __init__(self, sh, S, N, R, T, q_dtype, device, seed, shared_q=False):
         self.S, self.N, self.R, self.T, self.seed = S, N, R, T, seed
+        self.shared_q = shared_q
+        self._battery = None
         self.gids = (np.arange(sh.first, sh.first + S)[:, None] * N + np.arange(N)[None, :])
         self.q_dtype = q_dtype
         self._env = self._prof = self._mi = None
@@ -28,7 +30,7 @@ class OracleEngine:
         if self.ob is None:
             self.ob = OracleBatch(S=self.S, N=self.N, R=self.R, load_w=self._prof[0], pv_w=self._prof[1],
                                   max_in=self._mi, env_time=self._env[0], env_tout=self._env[1],
-                                  q_dtype=self.q_dtype)
+                                  q_dtype=self.q_dtype, shared_q=self.shared_q)
         return self.ob
 
     def set_temperatures(self, t_in, t_m):
@@ -46,3 +48,25 @@ class OracleEngine:
 
     def episode_reward(self):
         return self.last["episode_reward"]
+
+    def set_battery(self, capacity, min_soc=0.1, max_soc=0.9, efficiency=0.9, soc0=0.5):
+        ob = self._ensure()
+        ob.battery_capacity = np.broadcast_to(np.asarray(capacity, np.float64), (self.S, self.N)).copy()
+        ob.battery_bounds = (min_soc, max_soc, efficiency)
+        ob.soc = np.full((self.S, self.N), float(soc0))
+
+    def get_soc(self):
+        return self.ob.soc.copy()
+
+    def get_q_delta(self):
+        return self.ob.q_delta.copy()
+
+    def set_q_delta(self, d):
+        self.ob.q_delta[:] = np.asarray(d, np.int64).reshape(self.ob.q_delta.shape)
+
+    def apply_q_delta(self):
+        self.ob.apply_q_delta()
+
+    def get_q(self, first=0, count=None):
+        q = self.ob.q
+        return q[first:first + (len(q) - first if count is None else count)].copy()

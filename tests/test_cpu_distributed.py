@@ -20,18 +20,32 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, kw):
     import torch.distributed as dist
     from oracle_engine import OracleEngine
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    tr = ShardedTrainer(S_TOTAL, N, R, T, rank=rank, world=world, engine_factory=OracleEngine)
+    tr = ShardedTrainer(S_TOTAL, N, R, T, rank=rank, world=world, engine_factory=OracleEngine, **kw)
     means = [tr.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
     per_scen = tr.episode_rewards_global()
     if rank == 0:
-        q.put((means, per_scen))
+        q.put((means, per_scen, tr.eng.get_q(0, 1) if kw.get("shared_q") else None))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _run_two_ranks(kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, kw)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
 
 
 def test_shard_split():
@@ -46,15 +60,22 @@ def test_two_rank_gloo_matches_single_process():
     single = ShardedTrainer(S_TOTAL, N, R, T, engine_factory=OracleEngine)
     means1 = [single.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
     per1 = single.episode_rewards_global()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    means2, per2 = q.get(timeout=240)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    means2, per2, _ = _run_two_ranks({})
     assert np.array_equal(per1, per2)
+    assert np.allclose(means1, means2, rtol=0, atol=1e-9)
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shared_table_exchange_is_world_size_invariant():
+    """Config 3: one shared table, int64 deltas summed over the ranks (host exchange over gloo)
+    -> the table and every scenario's rewards equal the single-process run bit for bit."""
+    from oracle_engine import OracleEngine
+    kw = dict(shared_q=True, exchange="host", battery=dict(capacity=4.0e6 * 3600))
+    single = ShardedTrainer(S_TOTAL, N, R, T, engine_factory=OracleEngine, **kw)
+    means1 = [single.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    per1 = single.episode_rewards_global()
+    q1 = single.eng.get_q(0, 1)
+    assert np.count_nonzero(q1) > 0
+    means2, per2, q2 = _run_two_ranks(kw)
+    assert np.array_equal(per1, per2) and np.array_equal(q1, q2)
     assert np.allclose(means1, means2, rtol=0, atol=1e-9)

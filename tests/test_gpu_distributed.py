@@ -60,3 +60,40 @@ def test_two_ranks_match_single_context():
             rank, first, qloc = g
             assert np.array_equal(qloc, single.eng.get_q(first=first * N, count=4))
     single.eng.close()
+
+
+def _shared_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = ShardedTrainer(301, 4, 1, 96, rank=rank, world=world, device=0, shared_q=True, exchange="host",
+                        battery=dict(capacity=4.0e6 * 3600))
+    means = [tr.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    per = tr.episode_rewards_global()
+    if rank == 0:
+        q.put((means, per, tr.eng.get_q(0, 1)))
+    dist.barrier()
+    tr.eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_shared_table_two_ranks_match_single_context():
+    """Config 3 on the device: one shared table, deltas exchanged over the process group."""
+    single = ShardedTrainer(301, 4, 1, 96, device=0, shared_q=True, battery=dict(capacity=4.0e6 * 3600))
+    means1 = [single.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    per1, q1 = single.episode_rewards_global(), single.eng.get_q(0, 1)
+    single.eng.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shared_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    means2, per2, q2 = q.get(timeout=500)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.count_nonzero(q1) > 0
+    assert np.array_equal(per1, per2) and np.array_equal(q1, q2)
+    assert np.allclose(means1, means2, rtol=0, atol=1e-9)
