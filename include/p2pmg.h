@@ -56,6 +56,7 @@ typedef struct p2pmg_ctx p2pmg_ctx;
 
 #define P2PMG_MODE_TRAIN 0  /* train_episode: epsilon-greedy + TD update */
 #define P2PMG_MODE_GREEDY 1 /* run(): greedy actions, no update, no RNG */
+#define P2PMG_MODE_FILL 2   /* DQN init_buffers (community.py:125-147): act + store memory, no training */
 
 #define P2PMG_RNG_REPLAY 0 /* exploration codes supplied by the host (reference stream) */
 #define P2PMG_RNG_PHILOX 1 /* counter-keyed Philox4x32-10 on (seed, episode, agent, t, round) */
@@ -68,6 +69,7 @@ typedef struct p2pmg_ctx p2pmg_ctx;
 #define P2PMG_REC_TEMP 16    /* f32 [T][A] T_in before the step's RC update (heating.py:139) */
 #define P2PMG_REC_ACTION 32  /* u8  [T][R+1][A] action index (decisions, community.py:88-89) */
 #define P2PMG_REC_INDEX 64   /* i32 [T][R+1][A] packed state index it | iT<<8 | ib<<16 | ip<<24 */
+#define P2PMG_REC_LOSS 128   /* f32 [T][A] DQN loss of the agent's train step (rl.py:331) */
 
 #define P2PMG_GREEDY 255 /* replay code: no exploration in this (t, round, agent) */
 
@@ -108,9 +110,13 @@ typedef struct p2pmg_config {
   int32_t shared_q;        /* 0: one table per agent (the reference, rl.py:73);
                               1: one shared policy table for every agent of every scenario
                               (config 3, build-defined): frozen during an episode, TD deltas summed
-                              in int64 fixed point (2^-40) and applied by p2pmg_apply_q_delta */
-  int32_t reserved0;
+                              in int64 fixed point (2^-40) and applied by p2pmg_apply_q_delta;
+                              with learner = DQN: one shared Q-network (config 5, data-parallel) */
+  int32_t learner;         /* P2PMG_LEARNER_TABULAR (QAgent) | P2PMG_LEARNER_DQN (DQNAgent) */
 } p2pmg_config;
+
+#define P2PMG_LEARNER_TABULAR 0
+#define P2PMG_LEARNER_DQN 1
 
 typedef struct p2pmg_episode_args {
   int32_t mode;     /* P2PMG_MODE_TRAIN | P2PMG_MODE_GREEDY */
@@ -207,6 +213,49 @@ int p2pmg_q_calls(p2pmg_ctx* ctx, int n, const int32_t* agents, const float* s_o
  * eps for decision k is eps[k % n_eps].  Returns P2PMG_E_INVALID if the words run out. */
 int p2pmg_replay_decode(const uint32_t* words, size_t n_words, size_t n_decisions,
                         const double* eps, size_t n_eps, uint8_t* codes, size_t* consumed);
+
+/* ---- DQN variant (rl.py:135-359, agent.py:301-350; BASELINE.json configs[4]) -------------
+ * create with config.learner = P2PMG_LEARNER_DQN (no Q-table is allocated), then
+ * p2pmg_dqn_setup.  Per agent (or ONE network with config.shared_q = 1): online and target
+ * QNetwork 5->64->64->1 (Keras weight order, P2PMG_DQN_PARAMS floats), Adam state and a replay
+ * ring of `capacity` transitions (s[4], a, r, ns[4]).  p2pmg_run_episode dispatches to the DQN
+ * step pipeline: per timestep an act kernel (negotiation rounds with the Q-MLP, market, memory)
+ * then, in TRAIN mode, the train kernel (sample 32, target/online forward + backward on f32
+ * MFMA, clip, Adam, soft update). */
+#define P2PMG_DQN_PARAMS 4609
+#define P2PMG_DQN_ONLINE 0
+#define P2PMG_DQN_TARGET 1
+#define P2PMG_DQN_ADAM_M 2
+#define P2PMG_DQN_ADAM_V 3
+
+typedef struct p2pmg_dqn_config {
+  double gamma;    /* 0.95 agent.py:309 */
+  double tau;      /* 0.005 soft update agent.py:309 */
+  double lr;       /* 1e-5 Adam agent.py:310 */
+  double beta1, beta2, adam_eps; /* Keras Adam defaults .9, .999, 1e-7 */
+  double clip;     /* 1.0: first kernel's gradient clipped to [-clip, clip] (rl.py:329) */
+  int32_t batch;   /* 32 (agent.py:308); the only supported value */
+  int32_t capacity; /* 5000 (agent.py:308) */
+  int32_t agents_per_block; /* shared network: agents whose gradients one workgroup sums (0 = auto) */
+  int32_t reserved;
+} p2pmg_dqn_config;
+
+int p2pmg_dqn_config_default(p2pmg_dqn_config* cfg);
+int p2pmg_dqn_setup(p2pmg_ctx* ctx, const p2pmg_dqn_config* cfg);
+/* which = P2PMG_DQN_*; nets [first, first+count) of [count][P2PMG_DQN_PARAMS] f32 */
+int p2pmg_dqn_set_weights(p2pmg_ctx* ctx, int which, int first, int count, const float* host);
+int p2pmg_dqn_get_weights(p2pmg_ctx* ctx, int which, int first, int count, float* host);
+int p2pmg_dqn_set_step(p2pmg_ctx* ctx, int64_t step);   /* Adam iterations done (Keras `iterations`) */
+int p2pmg_dqn_get_step(p2pmg_ctx* ctx, int64_t* step);
+/* replay mode: deque indices (0 = oldest) of random.sample(buffer, 32) (rl.py:238) [T][A][32] */
+int p2pmg_dqn_set_samples(p2pmg_ctx* ctx, const uint16_t* samples);
+/* replay memory of agents [first, first+count): [count][capacity][10] f32 ring + added[count] */
+int p2pmg_dqn_get_buffer(p2pmg_ctx* ctx, int first, int count, float* host, int32_t* added);
+int p2pmg_dqn_set_buffer(p2pmg_ctx* ctx, int first, int count, const float* host, const int32_t* added);
+/* QNetwork.call (rl.py:147-148) of one network on n rows x = concat(state, action) [n][5] */
+int p2pmg_dqn_forward(p2pmg_ctx* ctx, int net, int n, const float* x, float* q);
+/* Trainer._train + update_targets (rl.py:307-359) of one network on a given batch [32][10] */
+int p2pmg_dqn_train_batch(p2pmg_ctx* ctx, int net, const float* batch, float* loss);
 
 #ifdef __cplusplus
 }

@@ -16,8 +16,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libp2pmg.so")
-SOURCES = ["p2pmg_kernels.hip", "p2pmg_runtime.cpp"]
-HEADERS = ["p2pmg_internal.h", os.path.join(ROOT, "include", "p2pmg.h")]
+SOURCES = ["p2pmg_kernels.hip", "p2pmg_dqn.hip", "p2pmg_runtime.cpp"]
+HEADERS = ["p2pmg_internal.h", "p2pmg_device.h", os.path.join(ROOT, "include", "p2pmg.h")]
 ARCH = os.environ.get("P2PMG_ARCH", "gfx950")
 
 

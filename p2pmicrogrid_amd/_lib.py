@@ -16,9 +16,12 @@ from . import _build
 P2PMG_OK = 0
 STATUS = {0: "OK", 1: "INVALID", 2: "HIP", 3: "NOMEM", 4: "STATE", 5: "UNSUPPORTED"}
 Q_F64, Q_F32 = 0, 1
-MODE_TRAIN, MODE_GREEDY = 0, 1
+MODE_TRAIN, MODE_GREEDY, MODE_FILL = 0, 1, 2
+LEARNER_TABULAR, LEARNER_DQN = 0, 1
+DQN_ONLINE, DQN_TARGET, DQN_ADAM_M, DQN_ADAM_V = 0, 1, 2, 3
+DQN_PARAMS = 4609
 RNG_REPLAY, RNG_PHILOX = 0, 1
-REC = {"reward": 1, "cost": 2, "grid": 4, "p2p": 8, "t_in": 16, "action": 32, "index": 64}
+REC = {"reward": 1, "cost": 2, "grid": 4, "p2p": 8, "t_in": 16, "action": 32, "index": 64, "loss": 128}
 GREEDY = 255
 
 EXPORTS = [
@@ -31,6 +34,9 @@ EXPORTS = [
     "p2pmg_reset_kernel_times", "p2pmg_q_calls", "p2pmg_set_hp_levels", "p2pmg_set_battery", "p2pmg_get_soc",
     "p2pmg_battery_seq", "p2pmg_apply_q_delta", "p2pmg_get_q_delta", "p2pmg_set_q_delta", "p2pmg_comm_unique_id", "p2pmg_comm_init",
     "p2pmg_allreduce_q_delta", "p2pmg_comm_destroy",
+    "p2pmg_dqn_config_default", "p2pmg_dqn_setup", "p2pmg_dqn_set_weights", "p2pmg_dqn_get_weights",
+    "p2pmg_dqn_set_step", "p2pmg_dqn_get_step", "p2pmg_dqn_set_samples", "p2pmg_dqn_get_buffer",
+    "p2pmg_dqn_set_buffer", "p2pmg_dqn_forward", "p2pmg_dqn_train_batch",
 ]
 
 
@@ -45,8 +51,14 @@ class Config(C.Structure):
         ("inv_rvent", C.c_float), ("one_minus_frad", C.c_float), ("frad", C.c_float), ("solar_gain", C.c_float),
         ("hp_cop", C.c_float), ("seconds_per_minute", C.c_float), ("time_slot", C.c_float),
         ("minutes_per_hour", C.c_float), ("kilo", C.c_float), ("penalty_weight", C.c_float),
-        ("seed", C.c_uint64), ("scenario_offset", C.c_int64), ("shared_q", C.c_int32), ("reserved0", C.c_int32),
+        ("seed", C.c_uint64), ("scenario_offset", C.c_int64), ("shared_q", C.c_int32), ("learner", C.c_int32),
     ]
+
+
+class DqnConfig(C.Structure):
+    _fields_ = [("gamma", C.c_double), ("tau", C.c_double), ("lr", C.c_double), ("beta1", C.c_double),
+                ("beta2", C.c_double), ("adam_eps", C.c_double), ("clip", C.c_double), ("batch", C.c_int32),
+                ("capacity", C.c_int32), ("agents_per_block", C.c_int32), ("reserved", C.c_int32)]
 
 
 class EpisodeArgs(C.Structure):
@@ -109,6 +121,17 @@ def _declare(lib):
         "p2pmg_comm_init": ([vp, vp, i32, i32], i32),
         "p2pmg_allreduce_q_delta": ([vp], i32),
         "p2pmg_comm_destroy": ([vp], i32),
+        "p2pmg_dqn_config_default": ([C.POINTER(DqnConfig)], i32),
+        "p2pmg_dqn_setup": ([vp, C.POINTER(DqnConfig)], i32),
+        "p2pmg_dqn_set_weights": ([vp, i32, i32, i32, vp], i32),
+        "p2pmg_dqn_get_weights": ([vp, i32, i32, i32, vp], i32),
+        "p2pmg_dqn_set_step": ([vp, C.c_int64], i32),
+        "p2pmg_dqn_get_step": ([vp, C.POINTER(C.c_int64)], i32),
+        "p2pmg_dqn_set_samples": ([vp, vp], i32),
+        "p2pmg_dqn_get_buffer": ([vp, i32, i32, vp, vp], i32),
+        "p2pmg_dqn_set_buffer": ([vp, i32, i32, vp, vp], i32),
+        "p2pmg_dqn_forward": ([vp, i32, i32, vp, vp], i32),
+        "p2pmg_dqn_train_batch": ([vp, i32, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

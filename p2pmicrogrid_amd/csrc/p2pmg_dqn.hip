@@ -1,0 +1,577 @@
+// p2pmg_dqn.hip — gfx950 kernels of the DQN variant (BASELINE.json configs[4]):
+//   QNetwork rl.py:135-148, ActorModel rl.py:151-197, ReplayBuffer rl.py:200-248,
+//   Trainer._train / _soft_update rl.py:307-359, DQNAgent agent.py:301-350.
+//
+// One environment step = two launches (plus, for one shared network, a reduce and an Adam launch):
+//   dqn_act_kernel<N>    one workgroup per scenario, ONE WAVE PER AGENT; lane j is hidden unit j
+//                        of the agent's Q-MLP (weights streamed as coalesced 256-B rows), the
+//                        R+1 Jacobi rounds exchange the proposal matrix through LDS, then market,
+//                        reward, replay-memory append and the RC update (community.py:67-93,
+//                        149-182; agent.py:200-213, 225-232; heating.py:37-56).
+//   dqn_train_kernel     one 4-wave workgroup per agent (or per run of agents when the network
+//                        is shared): samples 32 transitions, target forward over the 96 rows
+//                        (ns x 3 action values), online forward + backward over the 32 rows, all
+//                        on v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulation); wave w
+//                        owns output columns 16w..16w+15 of every 64-wide layer.  Per-agent
+//                        networks: clip + Adam + soft update fused in the epilogue; shared: the
+//                        workgroup's gradient sum is written as a partial.
+// Layouts (HBM): networks [n_nets][4672] f32 (Keras order W1[5][64] b1 W2[64][64] b2 W3[64] b3),
+// replay rings [A][cap][10] f32 (s[4], a, r, ns[4]), added [A].
+#include "p2pmg_internal.h"
+
+namespace p2pmg {
+namespace {
+#include "p2pmg_device.h"
+
+constexpr int kH = 64;
+constexpr int kB = kDqnBatch;
+constexpr int kLdsRow = 68;  // padded activation rows: an MFMA A-operand read (16 rows x 4 k) hits 64 banks
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float relu(float x) { return x > 0.0f ? x : 0.0f; }
+
+// butterfly sums: every participating lane ends with the bitwise-same total
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float sum16(float v) {  // over the 16 lanes of a row group
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float sum_groups(float v) {  // over the 4 row groups (same lane & 15)
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ----------------------------------------------------------------- act: one env step
+template <int N>
+__global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
+  const EpisodeParams& p = d.e;
+  __shared__ float shP[2][N * N];
+  __shared__ float4 shH[N][kH];
+  __shared__ float shR[N];
+  const int s = blockIdx.x;
+  const int i = threadIdx.x / kWave;
+  const int lane = threadIdx.x % kWave;
+  const int a = s * N + i;
+  const int t = d.t, T = p.T, tn = (t + 1 == T) ? 0 : t + 1;
+  const int R1 = p.R + 1, W = (R1 + 3) >> 2;
+  const size_t A = (size_t)p.A;
+  const int s_env = p.n_env == 1 ? 0 : s;
+  const float* e0 = p.env + ((size_t)t * p.n_env + s_env) * kEnvStride;
+  const float* e1 = p.env + ((size_t)tn * p.n_env + s_env) * kEnvStride;
+  const float time_t = e0[0], t_out = e0[1], buy = e0[2], inj = e0[3], p2pp = e0[4];
+  const float time_n = e1[0];
+  const float2 f0 = p.prof[(size_t)t * A + a], f1 = p.prof[(size_t)tn * A + a];
+  const float mi = p.max_in[a];
+  float tin = p.t_in[a], tm = p.t_m[a];
+  const float bal = (f0.x - f0.y) / mi;  // RLAgent._get_balance agent.py:172-176
+  const float baln = (f1.x - f1.y) / mi;
+  const float tnorm = (tin - p.setpoint) / p.margin;  // HPHeating.normalized_temperature heating.py:118-120
+  const float4 lv = p.hp_lv[a];
+  const float* th = d.theta + (size_t)(d.n_nets == 1 ? 0 : a) * kNetStride;
+  // this lane's hidden unit (rl.py:139-141): first-layer column, biases, output weight
+  const float w10 = th[kOffW1 + 0 * kH + lane], w11 = th[kOffW1 + 1 * kH + lane], w12 = th[kOffW1 + 2 * kH + lane],
+              w13 = th[kOffW1 + 3 * kH + lane], w14 = th[kOffW1 + 4 * kH + lane];
+  const float b1 = th[kOffB1 + lane], b2 = th[kOffB2 + lane], w3 = th[kOffW3 + lane], b3 = th[kOffB3];
+  const float* w2col = th + kOffW2 + lane;
+  const bool greedy_mode = p.mode == 1;
+
+  if (threadIdx.x < N * N) shP[0][threadIdx.x] = 0.0f;
+  __syncthreads();
+  int cur = 0, act = 0;
+  float hp = 0.0f, p2pf = 0.0f;
+  for (int r = 0; r < R1; ++r) {
+    const float* P = shP[cur];
+    // powers = -P[:, i], diagonal zeroed (community.py:76,81); p2p = mean / max_in (agent.py:203)
+    float acc = 0.0f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : P[j * N + i]));
+    p2pf = div_n<N>(acc) / mi;
+    int code = 255;  // ActorModel.select_action rl.py:174-183: explore draw, else greedy
+    if (!greedy_mode) {
+      if (p.rng == 0) {
+        code = (int)((p.codes[((size_t)t * W + (r >> 2)) * A + a] >> (8 * (r & 3))) & 0xFFu);
+      } else {
+        uint32_t c0 = (uint32_t)(t * R1 + r), c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
+                 c3 = kTagDecision;
+        philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
+        const double u = ((double)(c0 >> 5) * 67108864.0 + (double)(c1 >> 6)) * (1.0 / 9007199254740992.0);
+        code = u < p.eps ? (int)__umulhi(c2, 3u) : 255;
+      }
+    }
+    if (code == 255) {
+      // ActorModel.greedy_action rl.py:188-196: Q(obs, a) for a in (0, .5, 1), argmax (first max)
+      float z = p2pf * w13;
+      z = fmaf(bal, w12, z);
+      z = fmaf(tnorm, w11, z);
+      z = fmaf(time_t, w10, z);
+      const float h0 = relu(z + b1), h1 = relu(fmaf(0.5f, w14, z) + b1), h2 = relu((z + w14) + b1);
+      shH[i][lane] = make_float4(h0, h1, h2, 0.0f);
+      wave_lds_fence();
+      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+#pragma unroll 8
+      for (int k = 0; k < kH; ++k) {
+        const float wk = w2col[k * kH];
+        const float4 hk = shH[i][k];
+        a0 = fmaf(hk.x, wk, a0);
+        a1 = fmaf(hk.y, wk, a1);
+        a2 = fmaf(hk.z, wk, a2);
+      }
+      wave_lds_fence();
+      const float q0 = wave_sum(relu(a0 + b2) * w3) + b3;
+      const float q1 = wave_sum(relu(a1 + b2) * w3) + b3;
+      const float q2 = wave_sum(relu(a2 + b2) * w3) + b3;
+      act = 0;
+      float best = q0;
+      if (q1 > best) { best = q1; act = 1; }
+      if (q2 > best) act = 2;
+    } else {
+      act = code;
+    }
+    hp = act == 0 ? lv.x : (act == 1 ? lv.y : lv.z);  // heating.set_power(action) -> hp.power * max_power
+    // RLAgent._divide_power agent.py:186-195 on out = balance * max_in + hp (agent.py:210)
+    const float out = (bal * mi) + hp;
+    const float so = sgn(out);
+    float tot = 0.0f, fj = 0.0f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const float pw = -((j == i || r == 0) ? 0.0f : P[j * N + i]);
+      const float f = (so != sgn(pw)) ? pw : 0.0f;
+      tot = tot + f;
+      if (j == lane) fj = f;
+    }
+    tot = fabsf(tot);
+    if (lane < N) {
+      float v;
+      if (tot == 0.0f) v = div_n<N>(out * 1.0f);
+      else v = (lane == i) ? (tot == tot ? out * 0.0f : tot) : (out * fabsf(fj)) / tot;
+      shP[cur ^ 1][i * N + lane] = v;
+    }
+    if (lane == 0 && (p.record & 32)) p.rec_action[((size_t)t * R1 + r) * A + a] = (uint8_t)act;
+    __syncthreads();
+    cur ^= 1;
+  }
+  // CommunityMicrogrid._assign_powers community.py:45-54 (final P, diagonal kept)
+  const float* P = shP[cur];
+  float g = 0.0f, pp = 0.0f;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const float pij = P[i * N + j], pji = P[j * N + i];
+    const float si = sgn(pij);
+    const float ex = (si != sgn(pji)) ? si * fminf(fabsf(pij), fabsf(pji)) : 0.0f;
+    g = g + (pij - ex);
+    pp = pp + ex;
+  }
+  // _compute_costs community.py:56-65; RLAgent.get_reward agent.py:225-232 (pre-update T_in)
+  float cost = (g >= 0.0f) ? g * buy : g * inj;
+  cost = cost + pp * p2pp;
+  cost = (cost * p.slot) / p.mph;
+  cost = cost * p.kilo;
+  float pen = fmaxf(fmaxf(0.0f, p.lower - tin), fmaxf(0.0f, tin - p.upper));
+  pen = pen > 0.0f ? pen + 1.0f : 0.0f;
+  const float rw = -(cost + p.penw * pen);
+
+  if (p.mode != 1) {
+    // DQNAgent.save_memory agent.py:332-336 -> ReplayBuffer.add rl.py:208-212
+    const int32_t n_added = d.added[a];
+    float* slot = d.buf + ((size_t)a * d.cap + (size_t)(n_added % d.cap)) * kTrans;
+    if (lane < kTrans) {
+      const float av = act == 0 ? 0.0f : (act == 1 ? 0.5f : 1.0f);
+      float v;
+      switch (lane) {
+        case 0: v = time_t; break;
+        case 1: v = tnorm; break;
+        case 2: v = bal; break;
+        case 3: v = p2pf; break;
+        case 4: v = av; break;
+        case 5: v = rw; break;
+        case 6: v = time_n; break;
+        case 7: v = tnorm; break;  // next state: same (pre-update) temperature (community.py:161)
+        case 8: v = baln; break;
+        default: v = 0.0f / mi; break;  // next state p2p = mean(zeros) / max_in
+      }
+      slot[lane] = v;
+    }
+    if (lane == 0) d.added[a] = n_added + 1;
+  }
+  if (lane == 0) {
+    const size_t k = (size_t)t * A + a;
+    if (p.record & 1) p.rec_reward[k] = rw;
+    if (p.record & 2) p.rec_cost[k] = cost;
+    if (p.record & 4) p.rec_grid[k] = g;
+    if (p.record & 8) p.rec_p2p[k] = pp;
+    if (p.record & 16) p.rec_tin[k] = tin;
+    rc_update(p, t_out, hp, tin, tm);  // HPHeating.step heating.py:138-143
+    p.t_in[a] = tin;
+    p.t_m[a] = tm;
+    shR[i] = rw;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // avg_reward = sum_t mean_i r (community.py:179), canonical order
+    float m = 0.0f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = m + shR[j];
+    const float ep = (t == 0 ? 0.0f : d.ep_acc[s]) + div_n<N>(m);
+    d.ep_acc[s] = ep;
+    p.ep_reward[s] = ep;
+  }
+}
+
+// ----------------------------------------------------------------- train: Trainer._train
+__device__ __forceinline__ void adam_update(const DqnParams& d, float* th, float* tg, float* mm, float* vv, int idx,
+                                            float g) {
+  // Keras Adam (beta1 .9, beta2 .999, eps 1e-7) then Trainer._soft_update (rl.py:335-354)
+  float m = mm[idx], v = vv[idx], w = th[idx];
+  m = m + (g - m) * d.b1c;
+  v = v + (g * g - v) * d.b2c;
+  w = w - (m * d.lr_t) / (sqrtf(v) + d.adam_eps);
+  mm[idx] = m;
+  vv[idx] = v;
+  th[idx] = w;
+  tg[idx] = d.tau_c * tg[idx] + d.tau * w;
+}
+
+template <bool SHARED>
+__global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
+  __shared__ float smp[kB][kTrans];
+  __shared__ float H1t[3 * kB][kLdsRow];
+  __shared__ float H1o[kB][kLdsRow];
+  __shared__ float dZ2[kB][kLdsRow];
+  __shared__ float qpart[4][4 * kB];  // per-wave partial Q: rows 0..95 target (action x sample), 96..127 online
+  const EpisodeParams& p = d.e;
+  const int w = threadIdx.x / kWave, l = threadIdx.x % kWave;
+  const int c16 = l & 15, g4 = l >> 4;
+  const int col = 16 * w + c16;  // this lane's column of every 64-wide layer
+  const size_t A = (size_t)p.A;
+
+  f32x4 gW2[4], gW1;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) gW2[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  gW1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float gb1 = 0.0f, gb2 = 0.0f, gW3 = 0.0f, gb3 = 0.0f;
+  const int n_ag = d.batch ? 1 : d.apb;
+  int net = 0;
+
+  for (int ag = 0; ag < n_ag; ++ag) {
+    const int a = d.batch ? 0 : blockIdx.x * d.apb + ag;
+    if (!d.batch && a >= (int)A) break;  // block-uniform
+    net = d.batch ? d.net : (SHARED ? 0 : a);
+    const float* th = d.theta + (size_t)net * kNetStride;
+    const float* tg = d.target + (size_t)net * kNetStride;
+
+    // ReplayBuffer.sample_batch rl.py:226-241: 32 distinct transitions
+    if (d.batch) {
+      for (int k = threadIdx.x; k < kB * kTrans; k += 256) smp[k / kTrans][k % kTrans] = d.batch[k];
+    } else {
+      if (w == 0) {
+        const int n_added = d.added[a];
+        const int count = n_added < d.cap ? n_added : d.cap;
+        const int first = n_added - count;
+        int idx = 0;
+        if (d.samples) {
+          idx = l < kB ? (int)d.samples[((size_t)d.t * A + a) * kB + l] : 0;
+        } else {  // Philox + Floyd (oracle/philox.py::sample_draws)
+          uint32_t c0 = (uint32_t)d.t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
+                   c3 = kTagSample + (uint32_t)(l & 31);
+          philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
+          const int mj = count - kB + (l & 31);
+          const int rj = (int)__umulhi(c0, (uint32_t)(mj + 1));
+          idx = rj;
+          for (int j = 0; j < kB; ++j) {
+            const int r = __shfl(rj, j, 64);
+            const bool taken = __ballot(l < j && idx == r) != 0;
+            if (l == j) idx = taken ? count - kB + j : r;
+          }
+        }
+        if (l < kB) {
+          const float* src = d.buf + ((size_t)a * d.cap + (size_t)((first + idx) % d.cap)) * kTrans;
+#pragma unroll
+          for (int k = 0; k < kTrans; ++k) smp[l][k] = src[k];
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- layer 1 (K = 5 padded to 8): Z1 = X W1 + b1, 6 target + 2 online row tiles
+    const float bt0 = tg[kOffW1 + g4 * kH + col], bo0 = th[kOffW1 + g4 * kH + col];
+    const float bt1 = g4 == 0 ? tg[kOffW1 + 4 * kH + col] : 0.0f, bo1 = g4 == 0 ? th[kOffW1 + 4 * kH + col] : 0.0f;
+    const float b1t = tg[kOffB1 + col], b1o = th[kOffB1 + col];
+    unsigned z1mask = 0;  // online rows where z1 > 0 (ReLU derivative), bit 4 rt + r
+#pragma unroll
+    for (int rt = 0; rt < 6; ++rt) {
+      const int row = 16 * rt + c16, act = row / kB, b = row % kB;
+      const float av = act == 0 ? 0.0f : (act == 1 ? 0.5f : 1.0f);
+      f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      acc = mfma4(smp[b][6 + g4], bt0, acc);
+      acc = mfma4(g4 == 0 ? av : 0.0f, bt1, acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) H1t[16 * rt + 4 * g4 + r][col] = relu(acc[r] + b1t);
+    }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int b = 16 * rt + c16;
+      f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      acc = mfma4(smp[b][g4], bo0, acc);
+      acc = mfma4(g4 == 0 ? smp[b][4] : 0.0f, bo1, acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = acc[r] + b1o;
+        H1o[16 * rt + 4 * g4 + r][col] = relu(z);
+        if (z > 0.0f) z1mask |= 1u << (4 * rt + r);
+      }
+    }
+    __syncthreads();
+
+    // ---- layer 2: Z2 = H1 W2 + b2 (K = 64)
+    f32x4 at[6], ao[2];
+#pragma unroll
+    for (int rt = 0; rt < 6; ++rt) at[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    ao[0] = ao[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 4
+    for (int kk = 0; kk < 16; ++kk) {
+      const int k = 4 * kk + g4;
+      const float bt = tg[kOffW2 + k * kH + col], bo = th[kOffW2 + k * kH + col];
+#pragma unroll
+      for (int rt = 0; rt < 6; ++rt) at[rt] = mfma4(H1t[16 * rt + c16][k], bt, at[rt]);
+      ao[0] = mfma4(H1o[c16][k], bo, ao[0]);
+      ao[1] = mfma4(H1o[16 + c16][k], bo, ao[1]);
+    }
+    const float b2t = tg[kOffB2 + col], w3t = tg[kOffW3 + col];
+    const float b2o = th[kOffB2 + col], w3o = th[kOffW3 + col];
+#pragma unroll
+    for (int rt = 0; rt < 6; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float qp = sum16(relu(at[rt][r] + b2t) * w3t);
+        if (c16 == 0) qpart[w][16 * rt + 4 * g4 + r] = qp;
+      }
+    float h2o[2][4];
+    unsigned z2mask = 0;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = ao[rt][r] + b2o;
+        h2o[rt][r] = relu(z);
+        if (z > 0.0f) z2mask |= 1u << (4 * rt + r);
+        const float qp = sum16(h2o[rt][r] * w3o);
+        if (c16 == 0) qpart[w][3 * kB + 16 * rt + 4 * g4 + r] = qp;
+      }
+    __syncthreads();
+
+    // ---- targets y = r + gamma * max_a' Q_target(ns, a') and dL/dq (rl.py:314-331)
+    const float b3t = tg[kOffB3], b3o = th[kOffB3];
+    float dq[2][4];
+    float lsum = 0.0f, dqsum = 0.0f;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 16 * rt + 4 * g4 + r;
+        float qt[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int row = k * kB + b;
+          qt[k] = (((qpart[0][row] + qpart[1][row]) + qpart[2][row]) + qpart[3][row]) + b3t;
+        }
+        const int ro = 3 * kB + b;
+        const float q = (((qpart[0][ro] + qpart[1][ro]) + qpart[2][ro]) + qpart[3][ro]) + b3o;
+        const float y = smp[b][5] + d.gamma * fmaxf(fmaxf(qt[0], qt[1]), qt[2]);
+        const float diff = q - y;
+        dq[rt][r] = (2.0f / (float)kB) * diff;
+        lsum += diff * diff;
+        dqsum += dq[rt][r];
+      }
+    if (w == 0) {  // loss = mean (y - q)^2; lanes with c16 == 0 hold disjoint rows
+      const float ls = sum_groups(lsum), dqs = sum_groups(dqsum);
+      if (l == 0) {
+        const float loss = ls / (float)kB;
+        if (d.batch) d.loss_out[0] = loss;
+        else if (d.rec_loss) d.rec_loss[(size_t)d.t * A + a] = loss;
+        gb3 += dqs;
+      }
+    }
+
+    // ---- backward (own columns)
+    float dz2[2][4];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool on = (z2mask >> (4 * rt + r)) & 1u;
+        dz2[rt][r] = on ? dq[rt][r] * w3o : 0.0f;
+        gW3 += h2o[rt][r] * dq[rt][r];
+        gb2 += dz2[rt][r];
+        dZ2[16 * rt + 4 * g4 + r][col] = dz2[rt][r];
+      }
+    // dW2 = H1^T dZ2: the accumulator rows of dz2 are the K index (b = 16 rt + 4 g4 + r)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gW2[mt] = mfma4(H1o[16 * rt + 4 * g4 + r][16 * mt + c16], dz2[rt][r], gW2[mt]);
+    __syncthreads();
+    // dH1 = dZ2 W2^T (own columns m = col), then dZ1 = dH1 * [z1 > 0]; dW1 = X^T dZ1
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 4
+      for (int kk = 0; kk < 16; ++kk) {
+        const int j = 4 * kk + g4;
+        acc = mfma4(dZ2[16 * rt + c16][j], th[kOffW2 + col * kH + j], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 16 * rt + 4 * g4 + r;
+        const float dz1 = ((z1mask >> (4 * rt + r)) & 1u) ? acc[r] : 0.0f;
+        gb1 += dz1;
+        const float x = c16 < 5 ? smp[b][c16] : 0.0f;
+        gW1 = mfma4(x, dz1, gW1);
+      }
+    }
+    __syncthreads();  // every wave is done with this agent's LDS and with the online W2
+  }
+
+  gb1 = sum_groups(gb1);
+  gb2 = sum_groups(gb2);
+  gW3 = sum_groups(gW3);
+  const int net_out = net;
+  if constexpr (!SHARED) {
+    // Trainer._train epilogue: clip the first kernel's gradient, Adam, then update_targets
+    float* th = d.theta + (size_t)net_out * kNetStride;
+    float* tg = d.target + (size_t)net_out * kNetStride;
+    float* mm = d.adam_m + (size_t)net_out * kNetStride;
+    float* vv = d.adam_v + (size_t)net_out * kNetStride;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) adam_update(d, th, tg, mm, vv, kOffW2 + (16 * mt + 4 * g4 + r) * kH + col, gW2[mt][r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = 4 * g4 + r;
+      if (k < 5) adam_update(d, th, tg, mm, vv, kOffW1 + k * kH + col, fminf(fmaxf(gW1[r], -d.clip), d.clip));
+    }
+    if (g4 == 0) {
+      adam_update(d, th, tg, mm, vv, kOffB1 + col, gb1);
+      adam_update(d, th, tg, mm, vv, kOffB2 + col, gb2);
+      adam_update(d, th, tg, mm, vv, kOffW3 + col, gW3);
+    }
+    if (threadIdx.x == 0) adam_update(d, th, tg, mm, vv, kOffB3, gb3);
+  } else {
+    float* gp = d.grad + (size_t)blockIdx.x * kNetStride;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gp[kOffW2 + (16 * mt + 4 * g4 + r) * kH + col] = gW2[mt][r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * g4 + r < 5) gp[kOffW1 + (4 * g4 + r) * kH + col] = gW1[r];
+    if (g4 == 0) {
+      gp[kOffB1 + col] = gb1;
+      gp[kOffB2 + col] = gb2;
+      gp[kOffW3 + col] = gW3;
+    }
+    if (threadIdx.x == 0) gp[kOffB3] = gb3;
+  }
+}
+
+// shared network: sum the workgroup partials in a fixed order
+__global__ void dqn_reduce_kernel(const DqnParams d, int n_partials) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= kDqnParams) return;
+  float s = 0.0f;
+  for (int b = 0; b < n_partials; ++b) s += d.grad[(size_t)b * kNetStride + k];
+  d.gsum[k] = s;
+}
+
+// shared network: mean over every agent (all ranks after the all-reduce), clip, Adam, soft update
+__global__ void dqn_adam_shared_kernel(const DqnParams d) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= kDqnParams) return;
+  float g = d.gsum[k] * d.inv_agents;
+  if (k < kOffB1) g = fminf(fmaxf(g, -d.clip), d.clip);
+  adam_update(d, d.theta, d.target, d.adam_m, d.adam_v, k, g);
+}
+
+// QNetwork.call on explicit rows (object API, rl.py:147-148): one thread per row
+__global__ void dqn_forward_kernel(const float* __restrict__ th, int n, const float* __restrict__ x,
+                                   float* __restrict__ q) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  float xi[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) xi[k] = x[(size_t)r * 5 + k];
+  float h1[kH];
+#pragma unroll
+  for (int j = 0; j < kH; ++j) {
+    float z = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) z = fmaf(xi[k], th[kOffW1 + k * kH + j], z);
+    h1[j] = relu(z + th[kOffB1 + j]);
+  }
+  float out = 0.0f;
+  for (int j = 0; j < kH; ++j) {
+    float z = 0.0f;
+#pragma unroll 16
+    for (int k = 0; k < kH; ++k) z = fmaf(h1[k], th[kOffW2 + k * kH + j], z);
+    out = fmaf(relu(z + th[kOffB2 + j]), th[kOffW3 + j], out);
+  }
+  q[r] = out + th[kOffB3];
+}
+
+}  // namespace
+
+hipError_t launch_dqn_act(const DqnParams& d, hipStream_t st) {
+  const dim3 grid(d.e.S);
+  switch (d.e.N) {
+#define P2PMG_DQN_ACT(NN) \
+  case NN: hipLaunchKernelGGL(dqn_act_kernel<NN>, grid, dim3(NN * kWave), 0, st, d); break;
+    P2PMG_DQN_ACT(1) P2PMG_DQN_ACT(2) P2PMG_DQN_ACT(3) P2PMG_DQN_ACT(4) P2PMG_DQN_ACT(5) P2PMG_DQN_ACT(6)
+    P2PMG_DQN_ACT(7) P2PMG_DQN_ACT(8) P2PMG_DQN_ACT(16)
+#undef P2PMG_DQN_ACT
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_dqn_train(const DqnParams& d, int blocks, bool shared_partials, hipStream_t st) {
+  if (shared_partials)
+    hipLaunchKernelGGL(dqn_train_kernel<true>, dim3(blocks), dim3(256), 0, st, d);
+  else
+    hipLaunchKernelGGL(dqn_train_kernel<false>, dim3(blocks), dim3(256), 0, st, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_dqn_reduce(const DqnParams& d, int n_partials, hipStream_t st) {
+  hipLaunchKernelGGL(dqn_reduce_kernel, dim3((kDqnParams + 255) / 256), dim3(256), 0, st, d, n_partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_dqn_adam_shared(const DqnParams& d, hipStream_t st) {
+  hipLaunchKernelGGL(dqn_adam_shared_kernel, dim3((kDqnParams + 255) / 256), dim3(256), 0, st, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_dqn_forward(const float* theta, int n, const float* x, float* q, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dqn_forward_kernel, dim3((n + 127) / 128), dim3(128), 0, st, theta, n, x, q);
+  return hipGetLastError();
+}
+
+}  // namespace p2pmg

@@ -57,6 +57,43 @@ struct EpisodeParams {
   float mph, kilo, penw;
 };
 
+// ---- DQN variant (rl.py:135-359): QNetwork 5 -> 64 -> 64 -> 1 in Keras weight order
+constexpr int kNetStride = 4672;  // floats per network slot (4609 used; 64-float aligned)
+constexpr int kOffW1 = 0, kOffB1 = 320, kOffW2 = 384, kOffB2 = 4480, kOffW3 = 4544, kOffB3 = 4608;
+constexpr int kDqnParams = 4609;
+constexpr int kDqnBatch = 32;     // agent.py:308
+constexpr int kTrans = 10;        // floats per transition: s[4], a, r, ns[4]
+constexpr uint32_t kTagSample = 0x5EED0100u;  // + j: replay-buffer sample draws (oracle/philox.py)
+
+struct DqnParams {
+  EpisodeParams e;           // simulation inputs, state, records and constants (q unused)
+  int t;                     // timestep of this launch
+  int n_nets;                // A (per-agent networks, the reference) or 1 (shared, config 5)
+  float* theta;              // [n_nets][kNetStride] online network
+  float* target;             // [n_nets][kNetStride] target network
+  float* adam_m;
+  float* adam_v;
+  float* grad;               // shared: [blocks][kNetStride] partial sums; then the sum in row 0 of gsum
+  float* gsum;               // shared: [kNetStride]
+  float* buf;                // [A][cap][kTrans] replay rings
+  int32_t* added;            // [A] transitions ever added
+  int cap;
+  const uint16_t* samples;   // replay mode: [T][A][32] deque indices; null = Philox (Floyd)
+  float* rec_loss;           // [T][A] or null
+  float* ep_acc;             // [S] running sum_t mean_i r
+  float gamma, tau, tau_c, lr_t, b1c, b2c, adam_eps, clip;
+  float inv_agents;          // shared: 1 / (agents over all ranks)
+  int apb;                   // agents per train workgroup
+  const float* batch;        // explicit [32][kTrans] batch (p2pmg_dqn_train_batch) or null
+  int net;                   // network of the explicit batch
+  float* loss_out;           // explicit batch: [1]
+};
+hipError_t launch_dqn_act(const DqnParams& p, hipStream_t stream);
+hipError_t launch_dqn_train(const DqnParams& p, int blocks, bool shared_partials, hipStream_t stream);
+hipError_t launch_dqn_reduce(const DqnParams& p, int n_partials, hipStream_t stream);
+hipError_t launch_dqn_adam_shared(const DqnParams& p, hipStream_t stream);
+hipError_t launch_dqn_forward(const float* theta, int n, const float* x, float* q, hipStream_t stream);
+
 struct RcParams {
   float inv_ci, inv_cm, inv_ri, inv_re, inv_rvent, c_in, c_m, solar, cop, spm, slot;
 };

@@ -6,7 +6,9 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -52,7 +54,27 @@ struct p2pmg_ctx {
   double bat_min = 0.1, bat_max = 0.9, bat_sqrt_eff = 1.0;
   long long* qdelta = nullptr; // shared table deltas [kDeltaCopies][n_states][4]
   void* comm = nullptr;        // ncclComm_t
+  int nranks = 1;
   bool have_env = false, have_prof = false, have_params = false, have_codes = false;
+  // DQN learner (config.learner = P2PMG_LEARNER_DQN)
+  bool dqn = false;
+  p2pmg_dqn_config dcfg{};
+  int n_nets = 0;
+  float* d_theta = nullptr;   // [n_nets][kNetStride]
+  float* d_target = nullptr;
+  float* d_m = nullptr;
+  float* d_v = nullptr;
+  float* d_grad = nullptr;    // shared network: [d_blocks][kNetStride] partials
+  float* d_gsum = nullptr;    // [kNetStride]
+  int d_blocks = 0, d_apb = 1;
+  float* d_buf = nullptr;     // [A][capacity][10]
+  int32_t* d_added = nullptr; // [A]
+  uint16_t* d_samples = nullptr;  // [T][A][32]
+  bool have_samples = false;
+  float* d_ep_acc = nullptr;  // [S]
+  float* rec_loss = nullptr;  // [T][A]
+  int64_t d_step = 0;
+  int64_t d_added_min = 0;    // every ring holds at least this many transitions
   std::string err;
 };
 
@@ -135,6 +157,7 @@ int ensure_records(p2pmg_ctx* c, int mask) {
   const size_t tra = (size_t)c->T * (c->R + 1) * c->A;
   if ((mask & P2PMG_REC_ACTION) && !c->rec_action) HIP_TRY(c, dmalloc(&c->rec_action, tra));
   if ((mask & P2PMG_REC_INDEX) && !c->rec_index) HIP_TRY(c, dmalloc(&c->rec_index, tra));
+  if ((mask & P2PMG_REC_LOSS) && !c->rec_loss) HIP_TRY(c, dmalloc(&c->rec_loss, ta));
   return P2PMG_OK;
 }
 
@@ -228,10 +251,12 @@ int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
   const size_t ncw = (size_t)c->T * ((c->R + 4) / 4) * A;
   if (dmalloc(&c->codes, ncw) != hipSuccess) return bail(P2PMG_E_NOMEM);
   if (hipMemsetAsync(c->codes, 0xFF, ncw * 4, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
-  const size_t n_tables = cfg->shared_q ? 1 : A;
+  if (cfg->learner != P2PMG_LEARNER_TABULAR && cfg->learner != P2PMG_LEARNER_DQN) return bail(P2PMG_E_INVALID);
+  c->dqn = cfg->learner == P2PMG_LEARNER_DQN;
+  const size_t n_tables = c->dqn ? 0 : (cfg->shared_q ? 1 : A);
   const size_t qbytes = n_tables * c->n_states * kQPad * c->q_elem;
-  if (hipMalloc(&c->q, qbytes) != hipSuccess) return bail(P2PMG_E_NOMEM);
-  if (cfg->shared_q) {
+  if (hipMalloc(&c->q, qbytes ? qbytes : 16) != hipSuccess) return bail(P2PMG_E_NOMEM);
+  if (cfg->shared_q && !c->dqn) {
     if (dmalloc(&c->qdelta, p2pmg::kDeltaCopies * c->n_states * kQPad) != hipSuccess) return bail(P2PMG_E_NOMEM);
     if (hipMemsetAsync(c->qdelta, 0, p2pmg::kDeltaCopies * c->n_states * kQPad * 8, c->stream) != hipSuccess)
       return bail(P2PMG_E_HIP);
@@ -245,7 +270,7 @@ int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
         hipStreamSynchronize(c->stream) != hipSuccess)
       return bail(P2PMG_E_HIP);
   }
-  if (hipMemsetAsync(c->q, 0, qbytes, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
+  if (qbytes && hipMemsetAsync(c->q, 0, qbytes, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
   std::vector<float> t0(A, cfg->setpoint);
   if (hipMemcpyAsync(c->t_in, t0.data(), A * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(c->t_m, t0.data(), A * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
@@ -273,6 +298,17 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   dfree(c->soc);
   dfree(c->bat_cap);
   dfree(c->qdelta);
+  dfree(c->d_theta);
+  dfree(c->d_target);
+  dfree(c->d_m);
+  dfree(c->d_v);
+  dfree(c->d_grad);
+  dfree(c->d_gsum);
+  dfree(c->d_buf);
+  dfree(c->d_added);
+  dfree(c->d_samples);
+  dfree(c->d_ep_acc);
+  dfree(c->rec_loss);
   if (c->comm && rccl()) rccl()->commDestroy(c->comm);
   c->comm = nullptr;
   for (auto& ev : c->ring)
@@ -407,6 +443,7 @@ int p2pmg_set_replay_codes(p2pmg_ctx* c, const uint8_t* codes) {
 
 int p2pmg_zero_q(p2pmg_ctx* c) {
   if (!c) return P2PMG_E_INVALID;
+  if (c->dqn) return fail(c, P2PMG_E_STATE, "zero_q: DQN context has no Q-table");
   const size_t n_tables = c->cfg.shared_q ? 1 : (size_t)c->A;
   HIP_TRY(c, hipMemsetAsync(c->q, 0, n_tables * c->n_states * kQPad * c->q_elem, c->stream));
   if (c->qdelta) HIP_TRY(c, hipMemsetAsync(c->qdelta, 0, p2pmg::kDeltaCopies * c->n_states * kQPad * 8, c->stream));
@@ -414,6 +451,7 @@ int p2pmg_zero_q(p2pmg_ctx* c) {
 }
 
 static int q_range_ok(p2pmg_ctx* c, int first, int count, const void* host, int dtype) {
+  if (c && c->dqn) return 0;
   const int n_tables = c && c->cfg.shared_q ? 1 : (c ? c->A : 0);
   if (!c || !host || first < 0 || count < 0 || first + count > n_tables) return 0;
   return dtype == P2PMG_Q_F64 || dtype == P2PMG_Q_F32;
@@ -450,17 +488,8 @@ int p2pmg_get_q(p2pmg_ctx* c, int first, int count, void* host, int host_dtype) 
   return P2PMG_OK;
 }
 
-int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
-  if (!c || !args) return P2PMG_E_INVALID;
-  if (!c->have_env || !c->have_prof || !c->have_params)
-    return fail(c, P2PMG_E_STATE, "run_episode: env, profiles and agent params must be set first");
-  const bool train = args->mode == P2PMG_MODE_TRAIN;
-  if (args->mode != P2PMG_MODE_TRAIN && args->mode != P2PMG_MODE_GREEDY) return fail(c, P2PMG_E_INVALID, "mode");
-  if (train && args->rng != P2PMG_RNG_REPLAY && args->rng != P2PMG_RNG_PHILOX) return fail(c, P2PMG_E_INVALID, "rng");
-  if (train && args->rng == P2PMG_RNG_REPLAY && !c->have_codes)
-    return fail(c, P2PMG_E_STATE, "run_episode: replay mode needs p2pmg_set_replay_codes");
-  int rc = ensure_records(c, args->record);
-  if (rc != P2PMG_OK) return rc;
+static EpisodeParams episode_params(p2pmg_ctx* c, const p2pmg_episode_args* args) {
+  const bool train = args->mode != P2PMG_MODE_GREEDY;
   const p2pmg_config& g = c->cfg;
   EpisodeParams p{};
   p.S = c->S;
@@ -527,6 +556,25 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   p.mph = g.minutes_per_hour;
   p.kilo = g.kilo;
   p.penw = g.penalty_weight;
+  return p;
+}
+
+static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args);
+
+int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
+  if (!c || !args) return P2PMG_E_INVALID;
+  if (c->dqn) return dqn_run_episode(c, args);
+  if (!c->have_env || !c->have_prof || !c->have_params)
+    return fail(c, P2PMG_E_STATE, "run_episode: env, profiles and agent params must be set first");
+  const bool train = args->mode == P2PMG_MODE_TRAIN;
+  if (args->mode != P2PMG_MODE_TRAIN && args->mode != P2PMG_MODE_GREEDY) return fail(c, P2PMG_E_INVALID, "mode");
+  if (train && args->rng != P2PMG_RNG_REPLAY && args->rng != P2PMG_RNG_PHILOX) return fail(c, P2PMG_E_INVALID, "rng");
+  if (train && args->rng == P2PMG_RNG_REPLAY && !c->have_codes)
+    return fail(c, P2PMG_E_STATE, "run_episode: replay mode needs p2pmg_set_replay_codes");
+  int rc = ensure_records(c, args->record);
+  if (rc != P2PMG_OK) return rc;
+  EpisodeParams p = episode_params(c, args);
+  const p2pmg_config& g = c->cfg;
   if (train && args->rng == P2PMG_RNG_PHILOX) {
     bool prepass = c->A < (1 << 18);
     if (args->flags & P2PMG_FLAG_PHILOX_PREPASS) prepass = true;
@@ -603,6 +651,9 @@ int p2pmg_get_record(p2pmg_ctx* c, int which, void* host) {
   } else if (which == P2PMG_REC_INDEX) {
     src = c->rec_index;
     bytes = tra * 4;
+  } else if (which == P2PMG_REC_LOSS) {
+    src = c->rec_loss;
+    bytes = ta * 4;
   } else {
     return fail(c, P2PMG_E_INVALID, "get_record: unknown record");
   }
@@ -774,6 +825,7 @@ int p2pmg_comm_init(p2pmg_ctx* c, const uint8_t id[128], int rank, int nranks) {
   const int rc = r->commInitRank(&comm, nranks, uid, rank);
   if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclCommInitRank: ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
   c->comm = comm;
+  c->nranks = nranks;
   return P2PMG_OK;
 }
 
@@ -800,6 +852,7 @@ int p2pmg_q_calls(p2pmg_ctx* c, int n, const int32_t* agents, const float* s_obs
                   const float* rewards, const float* ns_obs, int train, int32_t* actions_out, double* q_out) {
   if (!c || n < 0 || !agents || !s_obs || !codes || !actions_out || !q_out) return P2PMG_E_INVALID;
   if (train && (!rewards || !ns_obs)) return fail(c, P2PMG_E_INVALID, "q_calls: train needs rewards and ns_obs");
+  if (c->dqn) return fail(c, P2PMG_E_STATE, "q_calls: DQN context has no Q-table");
   for (int k = 0; k < n; ++k)
     if (agents[k] < 0 || agents[k] >= c->A) return fail(c, P2PMG_E_INVALID, "q_calls: agent out of range");
   if (n == 0) return P2PMG_OK;
@@ -854,6 +907,307 @@ int p2pmg_replay_decode(const uint32_t* words, size_t n_words, size_t n_decision
     }
   }
   if (consumed) *consumed = pos;
+  return P2PMG_OK;
+}
+
+// ============================================================================ DQN learner
+int p2pmg_dqn_config_default(p2pmg_dqn_config* cfg) {
+  if (!cfg) return P2PMG_E_INVALID;
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->gamma = 0.95;  // agent.py:309
+  cfg->tau = 0.005;
+  cfg->lr = 1e-5;     // agent.py:310
+  cfg->beta1 = 0.9;
+  cfg->beta2 = 0.999;
+  cfg->adam_eps = 1e-7;
+  cfg->clip = 1.0;    // rl.py:329
+  cfg->batch = 32;    // agent.py:308
+  cfg->capacity = 5000;
+  cfg->agents_per_block = 0;
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_setup(p2pmg_ctx* c, const p2pmg_dqn_config* cfg) {
+  if (!c || !cfg) return P2PMG_E_INVALID;
+  if (!c->dqn) return fail(c, P2PMG_E_STATE, "dqn_setup: create the context with learner = P2PMG_LEARNER_DQN");
+  if (cfg->batch != p2pmg::kDqnBatch) return fail(c, P2PMG_E_UNSUPPORTED, "dqn_setup: batch must be 32");
+  if (cfg->capacity < p2pmg::kDqnBatch || cfg->capacity > 65535)
+    return fail(c, P2PMG_E_INVALID, "dqn_setup: capacity must be in [32, 65535]");
+  if (c->d_theta) return fail(c, P2PMG_E_STATE, "dqn_setup: already set up");
+  c->dcfg = *cfg;
+  const size_t A = (size_t)c->A, NS = p2pmg::kNetStride;
+  c->n_nets = c->cfg.shared_q ? 1 : c->A;
+  const size_t nn = (size_t)c->n_nets * NS;
+  HIP_TRY(c, dmalloc(&c->d_theta, nn));
+  HIP_TRY(c, dmalloc(&c->d_target, nn));
+  HIP_TRY(c, dmalloc(&c->d_m, nn));
+  HIP_TRY(c, dmalloc(&c->d_v, nn));
+  for (float* b : {c->d_theta, c->d_target, c->d_m, c->d_v}) HIP_TRY(c, hipMemsetAsync(b, 0, nn * 4, c->stream));
+  if (c->cfg.shared_q) {
+    int apb = cfg->agents_per_block > 0 ? cfg->agents_per_block : (int)((A + 2047) / 2048);
+    c->d_apb = apb < 1 ? 1 : apb;
+    c->d_blocks = (int)((A + c->d_apb - 1) / c->d_apb);
+    HIP_TRY(c, dmalloc(&c->d_grad, (size_t)c->d_blocks * NS));
+    HIP_TRY(c, dmalloc(&c->d_gsum, NS));
+  } else {
+    c->d_apb = 1;
+    c->d_blocks = c->A;
+  }
+  HIP_TRY(c, dmalloc(&c->d_buf, A * (size_t)cfg->capacity * p2pmg::kTrans));
+  HIP_TRY(c, dmalloc(&c->d_added, A));
+  HIP_TRY(c, hipMemsetAsync(c->d_added, 0, A * 4, c->stream));
+  HIP_TRY(c, dmalloc(&c->d_ep_acc, (size_t)c->S));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->d_step = 0;
+  c->d_added_min = 0;
+  return P2PMG_OK;
+}
+
+static float* dqn_array(p2pmg_ctx* c, int which) {
+  switch (which) {
+    case P2PMG_DQN_ONLINE: return c->d_theta;
+    case P2PMG_DQN_TARGET: return c->d_target;
+    case P2PMG_DQN_ADAM_M: return c->d_m;
+    case P2PMG_DQN_ADAM_V: return c->d_v;
+    default: return nullptr;
+  }
+}
+
+static int dqn_ready(p2pmg_ctx* c, const char* what) {
+  if (!c) return P2PMG_E_INVALID;
+  if (!c->dqn || !c->d_theta) return fail(c, P2PMG_E_STATE, std::string(what) + ": p2pmg_dqn_setup first");
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_set_weights(p2pmg_ctx* c, int which, int first, int count, const float* host) {
+  int rc = dqn_ready(c, "dqn_set_weights");
+  if (rc != P2PMG_OK) return rc;
+  float* dst = dqn_array(c, which);
+  if (!dst || !host || first < 0 || count < 0 || first + count > c->n_nets)
+    return fail(c, P2PMG_E_INVALID, "dqn_set_weights: bad array/range");
+  HIP_TRY(c, hipMemcpy2DAsync(dst + (size_t)first * p2pmg::kNetStride, p2pmg::kNetStride * 4, host,
+                              p2pmg::kDqnParams * 4, p2pmg::kDqnParams * 4, count, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_get_weights(p2pmg_ctx* c, int which, int first, int count, float* host) {
+  int rc = dqn_ready(c, "dqn_get_weights");
+  if (rc != P2PMG_OK) return rc;
+  const float* src = dqn_array(c, which);
+  if (!src || !host || first < 0 || count < 0 || first + count > c->n_nets)
+    return fail(c, P2PMG_E_INVALID, "dqn_get_weights: bad array/range");
+  HIP_TRY(c, hipMemcpy2DAsync(host, p2pmg::kDqnParams * 4, src + (size_t)first * p2pmg::kNetStride,
+                              p2pmg::kNetStride * 4, p2pmg::kDqnParams * 4, count, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_set_step(p2pmg_ctx* c, int64_t step) {
+  int rc = dqn_ready(c, "dqn_set_step");
+  if (rc != P2PMG_OK) return rc;
+  if (step < 0) return P2PMG_E_INVALID;
+  c->d_step = step;
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_get_step(p2pmg_ctx* c, int64_t* step) {
+  int rc = dqn_ready(c, "dqn_get_step");
+  if (rc != P2PMG_OK) return rc;
+  if (!step) return P2PMG_E_INVALID;
+  *step = c->d_step;
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_set_samples(p2pmg_ctx* c, const uint16_t* samples) {
+  int rc = dqn_ready(c, "dqn_set_samples");
+  if (rc != P2PMG_OK) return rc;
+  if (!samples) return P2PMG_E_INVALID;
+  const size_t n = (size_t)c->T * c->A * p2pmg::kDqnBatch;
+  if (!c->d_samples) HIP_TRY(c, dmalloc(&c->d_samples, n));
+  HIP_TRY(c, hipMemcpyAsync(c->d_samples, samples, n * 2, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->have_samples = true;
+  return P2PMG_OK;
+}
+
+static int dqn_refresh_added_min(p2pmg_ctx* c) {
+  std::vector<int32_t> h(c->A);
+  HIP_TRY(c, hipMemcpyAsync(h.data(), c->d_added, (size_t)c->A * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  int64_t m = INT64_MAX;
+  for (int32_t v : h) m = v < m ? v : m;
+  c->d_added_min = c->A ? m : 0;
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_get_buffer(p2pmg_ctx* c, int first, int count, float* host, int32_t* added) {
+  int rc = dqn_ready(c, "dqn_get_buffer");
+  if (rc != P2PMG_OK) return rc;
+  if (first < 0 || count < 0 || first + count > c->A) return fail(c, P2PMG_E_INVALID, "dqn_get_buffer: range");
+  const size_t per = (size_t)c->dcfg.capacity * p2pmg::kTrans;
+  if (host)
+    HIP_TRY(c, hipMemcpyAsync(host, c->d_buf + (size_t)first * per, (size_t)count * per * 4, hipMemcpyDeviceToHost,
+                              c->stream));
+  if (added)
+    HIP_TRY(c, hipMemcpyAsync(added, c->d_added + first, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_set_buffer(p2pmg_ctx* c, int first, int count, const float* host, const int32_t* added) {
+  int rc = dqn_ready(c, "dqn_set_buffer");
+  if (rc != P2PMG_OK) return rc;
+  if (first < 0 || count < 0 || first + count > c->A) return fail(c, P2PMG_E_INVALID, "dqn_set_buffer: range");
+  const size_t per = (size_t)c->dcfg.capacity * p2pmg::kTrans;
+  if (host)
+    HIP_TRY(c, hipMemcpyAsync(c->d_buf + (size_t)first * per, host, (size_t)count * per * 4, hipMemcpyHostToDevice,
+                              c->stream));
+  if (added)
+    HIP_TRY(c, hipMemcpyAsync(c->d_added + first, added, (size_t)count * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return dqn_refresh_added_min(c);
+}
+
+static p2pmg::DqnParams dqn_params(p2pmg_ctx* c, const EpisodeParams& e) {
+  p2pmg::DqnParams d{};
+  const p2pmg_dqn_config& q = c->dcfg;
+  d.e = e;
+  d.n_nets = c->n_nets;
+  d.theta = c->d_theta;
+  d.target = c->d_target;
+  d.adam_m = c->d_m;
+  d.adam_v = c->d_v;
+  d.grad = c->d_grad;
+  d.gsum = c->d_gsum;
+  d.buf = c->d_buf;
+  d.added = c->d_added;
+  d.cap = q.capacity;
+  d.samples = nullptr;
+  d.rec_loss = (e.record & P2PMG_REC_LOSS) ? c->rec_loss : nullptr;
+  d.ep_acc = c->d_ep_acc;
+  d.gamma = (float)q.gamma;
+  d.tau = (float)q.tau;
+  d.tau_c = 1.0f - (float)q.tau;
+  d.b1c = 1.0f - (float)q.beta1;
+  d.b2c = 1.0f - (float)q.beta2;
+  d.adam_eps = (float)q.adam_eps;
+  d.clip = (float)q.clip;
+  d.inv_agents = 1.0f / (float)((double)c->A * c->nranks);
+  d.apb = c->d_apb;
+  return d;
+}
+
+// Keras Adam step size for iteration `step` (1-based), float64 -> float32 (oracle/dqn.py::adam_lr)
+static float adam_lr(const p2pmg_dqn_config& q, int64_t step) {
+  const double t = (double)step;
+  return (float)(q.lr * std::sqrt(1.0 - std::pow(q.beta2, t)) / (1.0 - std::pow(q.beta1, t)));
+}
+
+static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d) {
+  c->d_step++;
+  d.lr_t = adam_lr(c->dcfg, c->d_step);
+  if (c->n_nets == 1) {
+    HIP_TRY(c, p2pmg::launch_dqn_train(d, c->d_blocks, true, c->stream));
+    HIP_TRY(c, p2pmg::launch_dqn_reduce(d, c->d_blocks, c->stream));
+    if (c->comm && c->nranks > 1) {
+      Rccl* r = rccl();
+      // ncclFloat32 = 7, ncclSum = 0: gradient sum over ranks (xGMI), 4609 floats
+      const int rc = r->allReduce(c->d_gsum, c->d_gsum, p2pmg::kDqnParams, 7, 0, c->comm, c->stream);
+      if (rc != 0) return fail(c, P2PMG_E_HIP, "dqn gradient all-reduce failed");
+    }
+    HIP_TRY(c, p2pmg::launch_dqn_adam_shared(d, c->stream));
+  } else {
+    HIP_TRY(c, p2pmg::launch_dqn_train(d, c->A, false, c->stream));
+  }
+  return P2PMG_OK;
+}
+
+static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
+  int rc = dqn_ready(c, "run_episode");
+  if (rc != P2PMG_OK) return rc;
+  const int mode = args->mode;
+  if (mode != P2PMG_MODE_TRAIN && mode != P2PMG_MODE_GREEDY && mode != P2PMG_MODE_FILL)
+    return fail(c, P2PMG_E_INVALID, "mode");
+  const bool acting = mode != P2PMG_MODE_GREEDY;
+  if (acting && args->rng != P2PMG_RNG_REPLAY && args->rng != P2PMG_RNG_PHILOX) return fail(c, P2PMG_E_INVALID, "rng");
+  if (acting && args->rng == P2PMG_RNG_REPLAY && !c->have_codes)
+    return fail(c, P2PMG_E_STATE, "run_episode: replay mode needs p2pmg_set_replay_codes");
+  if (mode == P2PMG_MODE_TRAIN && args->rng == P2PMG_RNG_REPLAY && !c->have_samples)
+    return fail(c, P2PMG_E_STATE, "run_episode: DQN replay training needs p2pmg_dqn_set_samples");
+  if (mode == P2PMG_MODE_TRAIN && c->d_added_min + 1 < p2pmg::kDqnBatch)
+    return fail(c, P2PMG_E_STATE, "run_episode: fill the replay memory first (>= 31 transitions per agent, "
+                                  "community.init_buffers)");
+  rc = ensure_records(c, args->record);
+  if (rc != P2PMG_OK) return rc;
+  EpisodeParams e = episode_params(c, args);
+  e.rng = (acting && args->rng == P2PMG_RNG_PHILOX) ? 1 : 0;
+  p2pmg::DqnParams d = dqn_params(c, e);
+  if (mode == P2PMG_MODE_TRAIN && args->rng == P2PMG_RNG_REPLAY) d.samples = c->d_samples;
+  if (c->ring.empty()) {
+    c->ring.assign(2 * p2pmg_ctx::kRing, nullptr);
+    for (auto& ev : c->ring) HIP_TRY(c, hipEventCreate(&ev));
+  }
+  const int slot = (int)(c->n_timed % p2pmg_ctx::kRing);
+  HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
+  HIP_TRY(c, hipEventRecord(c->ring[2 * slot], c->stream));
+  for (int t = 0; t < c->T; ++t) {
+    d.t = t;
+    d.e.mode = mode;
+    HIP_TRY(c, p2pmg::launch_dqn_act(d, c->stream));
+    if (mode == P2PMG_MODE_TRAIN) {
+      rc = dqn_train_step(c, d);
+      if (rc != P2PMG_OK) return rc;
+    }
+  }
+  HIP_TRY(c, hipEventRecord(c->ring[2 * slot + 1], c->stream));
+  HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  c->n_timed++;
+  if (acting) c->d_added_min += c->T;
+  if (acting && args->rng == P2PMG_RNG_REPLAY) c->have_codes = c->code_src == 1;
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_forward(p2pmg_ctx* c, int net, int n, const float* x, float* q) {
+  int rc = dqn_ready(c, "dqn_forward");
+  if (rc != P2PMG_OK) return rc;
+  if (net < 0 || net >= c->n_nets || n < 0 || (n > 0 && (!x || !q))) return fail(c, P2PMG_E_INVALID, "dqn_forward");
+  if (n == 0) return P2PMG_OK;
+  float *dx = nullptr, *dq = nullptr;
+  HIP_TRY(c, dmalloc(&dx, (size_t)n * 5));
+  hipError_t e = dmalloc(&dq, (size_t)n);
+  if (e == hipSuccess) e = hipMemcpyAsync(dx, x, (size_t)n * 20, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = p2pmg::launch_dqn_forward(c->d_theta + (size_t)net * p2pmg::kNetStride, n, dx, dq, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(q, dq, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(dx);
+  dfree(dq);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("dqn_forward: ") + hipGetErrorString(e));
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_train_batch(p2pmg_ctx* c, int net, const float* batch, float* loss) {
+  int rc = dqn_ready(c, "dqn_train_batch");
+  if (rc != P2PMG_OK) return rc;
+  if (net < 0 || net >= c->n_nets || !batch) return fail(c, P2PMG_E_INVALID, "dqn_train_batch");
+  float* db = nullptr;
+  HIP_TRY(c, dmalloc(&db, (size_t)p2pmg::kDqnBatch * p2pmg::kTrans + 1));
+  p2pmg_episode_args args{P2PMG_MODE_TRAIN, P2PMG_RNG_PHILOX, 0, 0, 0.0, 0, 0};
+  p2pmg::DqnParams d = dqn_params(c, episode_params(c, &args));
+  d.batch = db;
+  d.net = net;
+  d.loss_out = db + p2pmg::kDqnBatch * p2pmg::kTrans;
+  c->d_step++;
+  d.lr_t = adam_lr(c->dcfg, c->d_step);
+  hipError_t e = hipMemcpyAsync(db, batch, (size_t)p2pmg::kDqnBatch * p2pmg::kTrans * 4, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = p2pmg::launch_dqn_train(d, 1, false, c->stream);
+  float l = 0.0f;
+  if (e == hipSuccess) e = hipMemcpyAsync(&l, d.loss_out, 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(db);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("dqn_train_batch: ") + hipGetErrorString(e));
+  if (loss) *loss = l;
   return P2PMG_OK;
 }
 

@@ -1,0 +1,158 @@
+"""DQN variant (config 5) on the device vs the oracle (oracle/dqn.py).
+
+Tolerance (north_star): float32 Q values / weights within 1e-5 relative (summation order of the
+MFMA tiles differs from NumPy's), actions and all simulation quantities exact."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import dqn as odqn
+from oracle import philox
+from p2pmicrogrid_amd.dataset import scenario_batch
+from p2pmicrogrid_amd.dqn import DeviceDQNBatch
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+
+
+def _rel_close(got, want, rtol=RTOL, floor=1e-3):
+    """|got - want| <= rtol * max(|want|, floor * max|want|) elementwise."""
+    want = np.asarray(want, np.float64)
+    scale = np.maximum(np.abs(want), floor * np.abs(want).max())
+    err = np.abs(np.asarray(got, np.float64) - want) / scale
+    assert err.max() <= rtol, f"max rel err {err.max():.3g} at {np.unravel_index(err.argmax(), err.shape)}"
+
+
+def _q_scale(theta, x):
+    """fp32 yardstick of Q(x): magnitude of the summed terms sum_j |h2_j w3_j| + |b3| (a dot
+    product's rounding error scales with it, not with the possibly cancelled result)."""
+    _, (_, _, _, _, h2) = odqn.forward(theta, x)
+    p = odqn.unpack(theta)
+    return np.abs(h2) @ np.abs(p["W3"][..., 0]) + np.abs(p["b3"][0])
+
+
+def _q_close(got, theta, x, rtol=RTOL):
+    want, _ = odqn.forward(theta, x)
+    err = np.abs(np.asarray(got, np.float64) - want) / _q_scale(theta, x)
+    assert err.max() <= rtol, f"max scaled err {err.max():.3g}"
+
+
+def test_forward_matches_oracle():
+    eng = DeviceDQNBatch(1, 2, 1, 8, init_seed=3)
+    th = eng.get_weights("online")
+    x = np.random.RandomState(0).uniform(-1, 1, (500, 5)).astype(np.float32)
+    for net in (0, 1):
+        _q_close(eng.forward(x, net), th[net], x)
+    eng.close()
+
+
+def test_train_batch_matches_oracle_step():
+    eng = DeviceDQNBatch(1, 1, 1, 8, init_seed=4)
+    th = eng.get_weights("online")
+    tg = odqn.glorot_init(1, seed=9)
+    eng.set_weights("target", tg)
+    rs = np.random.RandomState(2)
+    m, v = np.zeros_like(th), np.zeros_like(th)
+    th_o, tg_o = th.copy(), tg.copy()
+    for k in range(3):
+        s = rs.uniform(-1, 1, (32, 4)).astype(np.float32)
+        ns = rs.uniform(-1, 1, (32, 4)).astype(np.float32)
+        a = odqn.ACTION_VALUES[rs.randint(0, 3, 32)]
+        r = rs.uniform(-3, 0, 32).astype(np.float32)
+        loss = eng.train_batch(s, a, r, ns)
+        g, lo = odqn.gradients(th_o, s[None], a[None], r[None], ns[None], tg_o, 0.95)
+        odqn.adam_step(th_o, m, v, g, k + 1)
+        odqn.soft_update(tg_o, th_o, 0.005)
+        assert abs(loss - lo[0]) <= 1e-5 * abs(lo[0])
+    assert eng.step == 3
+    # the updates are ~1e-5 of the weights: compare the update itself, relative to its size
+    _rel_close(eng.get_weights("online") - th, th_o - th, rtol=2e-3)
+    _rel_close(eng.get_weights("adam_m"), m, rtol=1e-4)
+    np.testing.assert_allclose(eng.get_weights("target"), tg_o, rtol=1e-6, atol=1e-9)
+    eng.close()
+
+
+def _pair(S, N, R, T, shared, init_seed=5):
+    inp = scenario_batch(S, N, T)
+    eng = DeviceDQNBatch(S, N, R, T, shared=shared, init_seed=init_seed)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    ob = odqn.OracleDQNBatch(S=S, N=N, R=R, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in,
+                             env_time=inp.time[None], env_tout=inp.t_out, theta0=eng.get_weights("online"),
+                             shared=shared)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    return eng, ob
+
+
+def _check_trained(eng, ob, th0):
+    """The learned networks: Q values on probe observations within 1e-5 relative; the weight
+    updates (~1e-3 of the weights after a few hundred Adam steps) within 1 % of their size."""
+    th, tg = eng.get_weights("online"), eng.get_weights("target")
+    _rel_close(th - th0, ob.theta - th0, rtol=1e-2, floor=1e-2)
+    probe = np.random.RandomState(7).uniform(-1, 1, (64, 4)).astype(np.float32)
+    x = np.concatenate([np.repeat(probe, 3, 0), np.tile(odqn.ACTION_VALUES, 64)[:, None]], 1)
+    for net in range(min(4, len(th))):
+        _q_close(eng.forward(x, net), ob.theta[net], x)  # device network vs oracle network
+        _q_close(odqn.forward(tg[net], x)[0], ob.target[net], x)
+
+
+def _reset(eng, ob, episode):
+    eng.reset_temperatures_philox(episode)
+    ob.t_in, ob.t_m = (x.reshape(ob.S, ob.N) for x in philox.t0_draws(42, episode, np.arange(ob.S * ob.N)))
+
+
+def _compare_episode(eng, out, mode, eps):
+    rec = eng.get_records(["reward", "cost", "grid", "p2p", "t_in", "action"] + (["loss"] if mode == "train" else []))
+    assert np.array_equal(rec["action"], out["action"].astype(np.uint8)), "actions differ"
+    for k in ("reward", "cost", "grid", "p2p", "t_in"):
+        assert np.array_equal(rec[k], out[k]), k
+    if mode == "train":
+        _rel_close(rec["loss"], out["loss"], rtol=1e-4)
+    assert np.array_equal(eng.episode_reward(), out["episode_reward"])
+
+
+@pytest.mark.parametrize("S,N,R,shared", [(3, 2, 1, False), (3, 2, 1, True), (2, 16, 1, False), (4, 3, 2, True)])
+def test_episodes_match_oracle(S, N, R, shared):
+    T = 48
+    eng, ob = _pair(S, N, R, T, shared)
+    th0 = ob.theta.copy()
+    ep = 0
+    for mode, eps in (("fill", 1.0), ("train", 0.9), ("train", 0.3)):
+        eng.run_episode(mode, "philox", episode=ep, epsilon=eps,
+                        record=("reward", "cost", "grid", "p2p", "t_in", "action", "loss"))
+        out = ob.run_episode(mode, rng="philox", episode=ep, eps=eps)
+        _compare_episode(eng, out, mode, eps)
+        buf, added = eng.get_buffer()
+        assert np.array_equal(added, ob.added.ravel())
+        assert np.array_equal(buf[:, :int(added.min())], ob.buf.reshape(S * N, -1, 10)[:, :int(added.min())])
+        ep += 1
+        _reset(eng, ob, ep)
+    _check_trained(eng, ob, th0)
+    eng.run_episode("greedy", record=("action", "reward"))
+    out = ob.run_episode("greedy")
+    assert np.array_equal(eng.get_record("action"), out["action"].astype(np.uint8))
+    eng.close()
+
+
+def test_reference_order_replay_thesis_community():
+    """S=1, N=2, R=1: exploration from Python's random + np.random.choice and buffer samples from
+    random.sample, generated in the reference's consumption order (oracle.dqn.reference_dqn_replay)."""
+    S, N, R, T = 1, 2, 1, 96
+    eng, ob = _pair(S, N, R, T, False)
+    th0 = ob.theta.copy()
+    py, npr = random.Random(42), np.random.RandomState(42)
+    codes, _ = odqn.reference_dqn_replay(py, npr, T, R, N, 1.0)
+    eng.set_replay_codes(codes[:, :, None, :])
+    eng.run_episode("fill", "replay", epsilon=1.0, record=("action",))
+    ob.run_episode("fill", codes=codes[:, :, None, :], rng="replay")
+    codes, samples = odqn.reference_dqn_replay(py, npr, T, R, N, 0.9, counts=ob.count().ravel())
+    eng.set_replay_codes(codes[:, :, None, :])
+    eng.set_samples(samples[:, None])
+    eng.run_episode("train", "replay", epsilon=0.9, record=("reward", "cost", "grid", "p2p", "t_in", "action", "loss"))
+    out = ob.run_episode("train", codes=codes[:, :, None, :], samples=samples[:, None], rng="replay")
+    _compare_episode(eng, out, "train", 0.9)
+    _check_trained(eng, ob, th0)
+    eng.close()
