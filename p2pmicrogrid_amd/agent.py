@@ -18,6 +18,7 @@ from . import setup
 from .dataset import ProfileDataset
 from .heating import Heating
 from .production import Production
+from . import rl
 from .rl import QActor
 from .storage import Storage
 
@@ -150,7 +151,28 @@ class QAgent(RLAgent):
         self._last_action: int = -1
 
 
+class DQNAgent(RLAgent):
+    """Deep Q-learning agent (agent.py:301-350): ActorModel(epsilon=1), Trainer with a 5000-entry
+    memory, batch 32, gamma 0.95, tau 0.005, Adam(1e-5).  Inside a CommunityMicrogrid its
+    networks, Adam state and memory are slot ``i`` of the community's DeviceDQNBatch."""
+
+    def __init__(self, *args, **kwargs) -> None:
+        super().__init__(rl.ActorModel(1), *args, **kwargs)
+        self.trainer = rl.Trainer(self.actor, buffer_size=5 * 1000, batch_size=32, gamma=0.95, tau=0.005,
+                                  optimizer=rl.Adam(learning_rate=1e-5))
+
+    def load_from_file(self, setting: str, implementation: str) -> None:
+        super().load_from_file(setting, implementation)
+        self.trainer.load_from_file(f'{re.sub("-", "_", setting)}_{self.id}', implementation)
+
+    def save_to_file(self, setting: str, implementation: str) -> None:
+        super().save_to_file(setting, implementation)
+        self.trainer.save_to_file(f'{re.sub("-", "_", setting)}_{self.id}', implementation)
+
+
 def agent_kind(agent) -> Optional[str]:
     if isinstance(agent, QAgent):
         return "tabular"
+    if isinstance(agent, DQNAgent):
+        return "dqn"
     return None

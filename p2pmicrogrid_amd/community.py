@@ -19,12 +19,12 @@ import numpy as np
 
 from . import dataset as ds
 from . import setup
-from .agent import ActingAgent, Agent, GridAgent, QAgent
+from .agent import ActingAgent, Agent, DQNAgent, GridAgent, QAgent, agent_kind
 from .engine import DeviceCommunityBatch, price_table
 from .environment import env
 from .heating import HeatPump, HPHeating
 from .production import PV, Prosumer
-from .rng import ReferenceRNG
+from .rng import ReferenceRNG, dqn_episode_draws, python_random
 from .storage import NoStorage
 
 F32 = np.float32
@@ -45,10 +45,37 @@ class CommunityMicrogrid:
         self._engine: Optional[DeviceCommunityBatch] = None
         self._uploaded: Dict[str, Any] = {}
         self._rng = ReferenceRNG()
+        kinds = {agent_kind(a) for a in agents}
+        if len(kinds) != 1 or None in kinds:
+            raise ValueError(f"a community needs agents of one learner kind, got {kinds}")
+        self._dqn = kinds == {"dqn"}
 
     # ------------------------------------------------------------ device state
+    def _new_dqn_engine(self, T, N):
+        from .dqn import DeviceDQNBatch
+        old = self._engine
+        carry = None
+        if old is not None:  # horizon changed: carry networks, Adam state and memories over
+            carry = ({w: old.get_weights(w) for w in ("adam_m", "adam_v")}, old.get_buffer(), old.step)
+            for a in self.agents:
+                a.actor.q_network.unbind()
+                a.trainer.target_network.unbind()
+            old.close()
+        eng = DeviceDQNBatch(1, N, self._rounds, T, device=self._device, init_seed=None)
+        for i, a in enumerate(self.agents):
+            a.trainer.bind(eng, i)
+        if carry is not None:
+            for w, v in carry[0].items():
+                eng.set_weights(w, v)
+            eng.set_buffer(*carry[1])
+            eng.step = carry[2]
+        return eng
+
     def _ensure_engine(self) -> DeviceCommunityBatch:
         T, N = len(env), len(self.agents)
+        if self._dqn and (self._engine is None or self._engine.T != T):
+            self._engine = self._new_dqn_engine(T, N)
+            self._uploaded = {}
         if self._engine is None or self._engine.T != T:
             if self._engine is not None:  # horizon changed: carry the learned tables over
                 tables = self._engine.get_q()
@@ -91,7 +118,10 @@ class CommunityMicrogrid:
 
     # ------------------------------------------------------------ the reference API
     def train_episode(self, all_rewards=None, all_losses=None, _rewards=None, _losses=None) -> Tuple[float, float]:
-        """community.py:149-182: one training episode; returns (sum_t mean_i reward, 0 loss)."""
+        """community.py:149-182: one training episode; returns (sum_t mean_i reward, mean loss)
+        (the loss is 0 for tabular agents, agent.py:298)."""
+        if self._dqn:
+            return self._train_episode_dqn()
         eng = self._ensure_engine()
         T, N = eng.T, eng.N
         self._push_temperatures(eng)
@@ -124,11 +154,46 @@ class CommunityMicrogrid:
         power = (r["grid"][:, 0, :] + r["p2p"][:, 0, :]).astype(F32)
         return power, r["cost"][:, 0, :]
 
+    # ------------------------------------------------------------ DQN agents
+    def _counts(self, eng):
+        _, added = eng.get_buffer()
+        return np.minimum(added, eng.capacity)
+
+    def _train_episode_dqn(self) -> Tuple[float, float]:
+        eng = self._ensure_engine()
+        T, N = eng.T, eng.N
+        self._push_temperatures(eng)
+        eps = [a.actor._epsilon for a in self.agents]
+        codes, samples = dqn_episode_draws(python_random(), self._rng.rs, T, self._rounds, N, eps,
+                                           counts=self._counts(eng))
+        eng.set_replay_codes(codes)
+        eng.set_samples(samples)
+        eng.run_episode("train", "replay", epsilon=float(eps[0]), record=("reward", "action", "loss"))
+        self._pull_records(eng, T)
+        self.last_rewards = eng.get_record("reward")[:, 0, :]
+        self.last_losses = eng.get_record("loss")[:, 0, :]
+        avg_reward = float(eng.episode_reward()[0])
+        for agent in self.agents:
+            agent.reset()
+        return avg_reward, float(np.mean(self.last_losses, dtype=np.float32))
+
     def init_buffers(self) -> None:
-        """community.py:125-147 fills DQN replay buffers; tabular agents have none."""
-        if any(isinstance(a, QAgent) for a in self.agents):
+        """community.py:125-147: five episodes of memory with the exploring actors (no training),
+        then Trainer.initialize_target per agent.  Tabular agents have no memory."""
+        if not self._dqn:
             return
-        raise NotImplementedError("DQN agents are not available in this build yet")
+        eng = self._ensure_engine()
+        T, N = eng.T, eng.N
+        for _ in range(5):
+            self._push_temperatures(eng)
+            eps = [a.actor._epsilon for a in self.agents]
+            codes, _ = dqn_episode_draws(python_random(), self._rng.rs, T, self._rounds, N, eps)
+            eng.set_replay_codes(codes)
+            eng.run_episode("fill", "replay", epsilon=float(eps[0]))
+            for agent in self.agents:
+                agent.reset()
+        for agent in self.agents:
+            agent.trainer.initialize_target()
 
     def _step(self) -> None:
         for agent in self.agents:
@@ -170,9 +235,12 @@ def get_community(agent_constructor: Callable[..., ActingAgent], n_agents: int,
 
 
 def get_rl_based_community(n_agents: int, homogeneous: bool) -> CommunityMicrogrid:
+    """community.py:240-245"""
     if setup.implementation == 'tabular':
         return get_community(QAgent, n_agents, homogeneous=homogeneous)
-    raise NotImplementedError(f"implementation {setup.implementation!r} is not available in this build")
+    if setup.implementation == 'dqn':
+        return get_community(DQNAgent, n_agents, homogeneous=homogeneous)
+    raise ValueError(f"unknown implementation {setup.implementation!r}")
 
 
 def setting_name(nr_agents=None, rounds=None, homogeneous=None) -> str:
@@ -192,17 +260,22 @@ def main(load_agents: bool = False, episodes: Optional[int] = None, save: bool =
     if load_agents:
         for agent in community.agents:
             agent.load_from_file(setting, setup.implementation)
+    if setup.implementation == 'dqn':
+        community.init_buffers()  # community.py:265-267
     rewards_q: collections.deque = collections.deque(maxlen=setup.min_episodes_criterion)
+    errors_q: collections.deque = collections.deque(maxlen=setup.min_episodes_criterion)
     history = []
     t0 = time.time()
     last = setup.max_episodes if episodes is None else setup.starting_episodes + episodes
     for episode in range(setup.starting_episodes, last):
         reward, error = community.train_episode()
         rewards_q.append(reward)
+        errors_q.append(error)
         history.append(reward)
         if episode % setup.min_episodes_criterion == 0:
             if verbose:
-                print(f'Average reward: {statistics.mean(rewards_q):.3f}. Average error: {0.0:.3f}')
+                print(f'Average reward: {statistics.mean(rewards_q):.3f}. '
+                      f'Average error: {statistics.mean(errors_q):.3f}')
             for agent in community.agents:
                 agent.actor.decay_exploration()
         if save and (episode + 1) % setup.save_episodes == 0:

@@ -80,3 +80,33 @@ class ReferenceRNG:
         if used.value:
             self.rs.randint(0, 2 ** 32, size=used.value, dtype=np.uint32)
         return codes.reshape(T, R + 1, N)
+
+
+def python_random():
+    """The module-level ``random`` generator the reference seeds in rl.py:25 and draws from in
+    ActorModel.select_action (rl.py:175) and ReplayBuffer.sample_batch (rl.py:238)."""
+    import random
+    return random._inst
+
+
+def dqn_episode_draws(py_rng, np_rs: np.random.RandomState, T: int, R: int, N: int, eps: Sequence[float],
+                      counts: Optional[Sequence[int]] = None, capacity: int = 5000, batch: int = 32):
+    """One DQN community episode's draws in the reference's consumption order:
+    per (t, round, agent): ``random.random() < eps`` then, exploring, ``np.random.choice([0, 1, 2])``
+    (rl.py:175-186); then per agent, after its transition was stored, ``random.sample(buffer, 32)``
+    (rl.py:238, only when ``counts`` - buffer sizes before the episode - is given).
+    Returns (codes uint8 [T, R+1, N], samples uint16 [T, N, 32] or None)."""
+    eps = np.broadcast_to(np.asarray(eps, np.float64), (N,))
+    codes = np.full((T, R + 1, N), _lib.GREEDY, np.uint8)
+    samples = None if counts is None else np.zeros((T, N, batch), np.uint16)
+    cnt = None if counts is None else [int(c) for c in counts]
+    for t in range(T):
+        for r in range(R + 1):
+            for i in range(N):
+                if py_rng.random() < eps[i]:
+                    codes[t, r, i] = np_rs.choice([0, 1, 2])
+        if samples is not None:
+            for i in range(N):
+                cnt[i] = min(cnt[i] + 1, capacity)
+                samples[t, i] = py_rng.sample(range(cnt[i]), min(cnt[i], batch))
+    return codes, samples
