@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define P2PMG_ABI_VERSION 1
+#define P2PMG_ABI_VERSION 2
 
 typedef struct p2pmg_ctx p2pmg_ctx;
 
@@ -125,7 +125,8 @@ typedef struct p2pmg_episode_args {
   int32_t record;   /* P2PMG_REC_* mask */
   double epsilon;   /* exploration rate shared by every agent (QActor._epsilon) */
   int32_t flags;    /* P2PMG_FLAG_* (0 = automatic choice) */
-  int32_t reserved;
+  int32_t scen_per_wave; /* fast kernel: scenarios per 64-lane wave (0 = automatic: 64 / pow2ceil(N)) */
+  double reset_sigma;    /* with P2PMG_FLAG_RESET_T0: sigma of the T0 draw */
 } p2pmg_episode_args;
 
 /* Philox placement: a parallel pre-pass writing per-step code words (latency-bound batches:
@@ -133,6 +134,14 @@ typedef struct p2pmg_episode_args {
  * bound batches: no extra HBM traffic).  Automatic: pre-pass below 2^18 agents.  Same stream. */
 #define P2PMG_FLAG_PHILOX_PREPASS 1
 #define P2PMG_FLAG_PHILOX_INKERNEL 2
+/* Kernel choice.  Automatic: the fast per-agent-table kernel (step pre-pass + rounds unrolled at
+ * compile time) whenever it applies (N <= 8, R + 1 <= 4, no battery, no shared table, in-range
+ * max_in); GENERAL forces the general episode kernel (same results, bit for bit). */
+#define P2PMG_FLAG_GENERAL_KERNEL 4
+/* End the episode with HPHeating.reset (community.py:181 -> heating.py:145-152): T0 for episode + 1
+ * drawn as p2pmg_reset_temperatures_philox(ctx, episode + 1, reset_sigma) would, fused into the
+ * episode (no extra launch). */
+#define P2PMG_FLAG_RESET_T0 8
 
 /* version / defaults */
 int p2pmg_abi_version(void);

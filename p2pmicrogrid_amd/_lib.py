@@ -63,10 +63,11 @@ class DqnConfig(C.Structure):
 
 class EpisodeArgs(C.Structure):
     _fields_ = [("mode", C.c_int32), ("rng", C.c_int32), ("episode", C.c_int32), ("record", C.c_int32),
-                ("epsilon", C.c_double), ("flags", C.c_int32), ("reserved", C.c_int32)]
+                ("epsilon", C.c_double), ("flags", C.c_int32), ("scen_per_wave", C.c_int32),
+                ("reset_sigma", C.c_double)]
 
 
-FLAG_PHILOX_PREPASS, FLAG_PHILOX_INKERNEL = 1, 2
+FLAG_PHILOX_PREPASS, FLAG_PHILOX_INKERNEL, FLAG_GENERAL_KERNEL, FLAG_RESET_T0 = 1, 2, 4, 8
 
 
 class P2PMGError(RuntimeError):
@@ -158,7 +159,7 @@ def lib() -> C.CDLL:
             raise P2PMGError(f"libp2pmg.so not found at {path}; run `python -m p2pmicrogrid_amd._build`")
         _lib = C.CDLL(path)
         _declare(_lib)
-        if _lib.p2pmg_abi_version() != 1:
+        if _lib.p2pmg_abi_version() != 2:
             raise P2PMGError("libp2pmg ABI version mismatch")
         return _lib
 

@@ -49,6 +49,10 @@ struct EpisodeParams {
   const double* bat_cap;     // [A] capacity in J (0 = no battery)
   double bat_min, bat_max, bat_sqrt_eff;
   const float4* hp_lv;       // [A] per-agent heat-pump power of actions 0..2 (agent.py:268, heating.py:124)
+  void* dummy;               // >= 2 * kWave * 32 B scratch: target of the fast kernel's masked-off stores
+  uint32_t* pre_ipc;         // fast path, N = 2: [T][A] round-1 p2p bins for the partner's 3 round-0 actions
+  int reset_t0;              // fast path: draw T0 for episode + 1 at the end (P2PMG_FLAG_RESET_T0)
+  double reset_sigma;
   int nt, nT, nb, np;
   double alpha, gamma;
   float hp_levels[4];
@@ -99,6 +103,25 @@ struct RcParams {
 };
 
 hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream);
+// fast per-agent-table path: step pre-pass ([T][A] {balw, bins}; optionally the Philox code
+// words) + episode_fast_kernel (N <= 8, R + 1 <= 4, no battery, no shared table)
+// Where one step pre-pass writes: its buffers and the episode its Philox draws are for.
+struct PrepOut {
+  uint2* pre;      // [T][A]
+  uint32_t* ipc;   // [T][A] or null (N != 2)
+  uint32_t* words; // [T][W][A] or null (no Philox draws)
+  int episode;
+};
+hipError_t launch_step_prepass(const EpisodeParams& p, const PrepOut& o, hipStream_t stream);
+// next != null: the launch also runs the step pre-pass of the next episode (episode p.episode + 1,
+// same epsilon) into *next, in extra workgroups beside the episode's own
+// ev0 / ev1: timing events stamped by the dispatch (hipExtLaunchKernel)
+hipError_t launch_episode_fast(const EpisodeParams& p, const uint2* pre, void* recs, int q_dtype, int spw,
+                               const PrepOut* next, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
+constexpr size_t kFastRecBytes = 32;  // one packed record row per agent-step (FastRec)
+// which: 0..4 reward, cost, grid, p2p, tin ([T][A] f32); 5 action (u8), 6 index (i32) [T][R+1][A]
+hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void* recs, int which, void* out,
+                                  hipStream_t stream);
 hipError_t launch_apply_delta(void* q, long long* qdelta, size_t n, int q_dtype, hipStream_t stream);
 hipError_t launch_fold_delta(long long* qdelta, size_t n, hipStream_t stream);
 hipError_t launch_battery_seq(int agents, int steps, const double* bal, double* out_bal, double* soc_hist,

@@ -14,6 +14,10 @@
 // lanes inside one wave (64 / G scenarios per wave, one wave per workgroup); the Jacobi
 // proposal matrix P never leaves the chip — each lane keeps its row in registers and reads
 // its column through a per-wave LDS tile (community.py:75-86).
+#include <hip/hip_ext.h>
+
+#include <algorithm>
+
 #include "p2pmg_internal.h"
 
 namespace p2pmg {
@@ -317,6 +321,14 @@ struct Patch {
   QT val;
 };
 template <typename QT>
+__device__ __forceinline__ Row4<QT> sel_row(int b, const Row4<QT>& x0, const Row4<QT>& x1, const Row4<QT>& x2) {
+  Row4<QT> r;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) r.v[k] = sel3(b, x0.v[k], x1.v[k], x2.v[k]);
+  r.v[3] = (QT)0;
+  return r;
+}
+template <typename QT>
 __device__ __forceinline__ Row4<QT> patched(Row4<QT> r, uint32_t addr, const Patch<QT>& pt) {
   if (pt.row == addr) {
 #pragma unroll
@@ -362,6 +374,12 @@ __device__ __forceinline__ void lds_add_by_key(uint32_t* hk, unsigned long long*
   atomicAdd(gbase + key, (unsigned long long)v);  // crowded table: straight to the global replica
 }
 
+// timing-only ablations of the fast kernel's gathers: 7 = round-R gather fake, 8 = prefetched rows fake
+template <typename QT>
+__device__ __forceinline__ Row4<QT> fake_row(const QT* p) {
+  const uint32_t x = (uint32_t)(reinterpret_cast<uintptr_t>(p) >> 5);
+  return Row4<QT>{{(QT)(x & 3), (QT)((x >> 2) & 3), (QT)((x >> 4) & 3), (QT)0}};
+}
 template <typename QT>
 __device__ __forceinline__ Row4<QT> gather_row(const QT* p) {
 #if P2PMG_ABLATE == 1 || P2PMG_ABLATE == 4
@@ -713,6 +731,546 @@ __global__ void pack_codes_kernel(int T, int R1, int A, const uint8_t* __restric
   }
 }
 
+// ----------------------------------------------------------------- the fast per-agent-table path
+// IEEE f32 division a / b without its range handling.  hipcc's correctly rounded sequence is
+//   v_div_scale(b), v_rcp, y = fma(fma(-b, rcp, 1), rcp, rcp), v_div_scale(a),
+//   q = a*y, r = fma(-b, q, a), q = fma(r, y, q), r = fma(-b, q, a), v_div_fmas = fma(r, y, q),
+//   v_div_fixup
+// The two scale steps are identities (and v_div_fmas a plain fma) while |a| and |b| lie in
+// [2^-40, 2^40] (exponent gap below 96, nothing near denormal or overflow), and v_div_fixup only
+// rewrites NaN / inf / zero / denormal cases, none of which a quotient of two such numbers is.
+// So inside that range these five ops ARE the division, bit for bit; outside it, or for a = 0,
+// the caller takes the IEEE operator.  The reciprocal of a loop-invariant divisor (max_in, the
+// 60 minutes of an hour, N, the comfort margin) is hoisted out of the episode loop.
+struct Recip {
+  float b, y;
+  bool ok;  // |b| in range
+};
+__device__ __forceinline__ bool in_div_range(float x) {
+  const float m = fabsf(x);
+  return m >= 0x1p-40f && m <= 0x1p40f;
+}
+__device__ __forceinline__ Recip recip(float b) {
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  return Recip{b, __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0), in_div_range(b)};
+}
+__device__ __forceinline__ float fdiv_core(float a, const Recip& d) {
+  const float q0 = a * d.y;
+  float r = __builtin_fmaf(-d.b, q0, a);
+  float q = __builtin_fmaf(r, d.y, q0);
+  r = __builtin_fmaf(-d.b, q, a);
+  q = __builtin_fmaf(r, d.y, q);
+  // a = +-0: the steps above give +0; the IEEE quotient carries sign(a) * sign(b) = sign(q0).
+  // For every other a the sign of q already equals sign(q0), so the copy is exact either way.
+  return __builtin_copysignf(q, q0);
+}
+__device__ __forceinline__ bool fdiv_ok(float a) {
+  const float m = fabsf(a);
+  return (m >= 0x1p-40f && m <= 0x1p40f) || m == 0.0f;
+}
+// the IEEE quotient behind an opaque copy of a: keeps the compiler from speculating this rare path
+// (11 instructions) into a select on the common one
+__device__ __forceinline__ float fdiv_ieee(float a, float b) {
+  asm volatile("" : "+v"(a));
+  return a / b;
+}
+// a / b with a divisor the launcher has checked to lie in range (max_in, 60, N, the margin)
+__device__ __forceinline__ float fdiv_b(float a, const Recip& d) {
+  float q = fdiv_core(a, d);
+  if (!fdiv_ok(a)) q = fdiv_ieee(a, d.b);  // rare: tiny, huge or non-finite numerator
+  return q;
+}
+template <int N>
+__device__ __forceinline__ float div_n_r(float x, const Recip& rn) {
+  if constexpr ((N & (N - 1)) == 0) return x * (1.0f / (float)N);
+  else return fdiv_b(x, rn);
+}
+// clamp_bin as one v_med3: (int)med3(v, 0, K-1) equals clamp_bin for every non-NaN v (values in
+// [0, 1) truncate to 0 like the reference's v < 1 branch)
+__device__ __forceinline__ int clamp_bin_f(float v, float km1) { return (int)__builtin_amdgcn_fmed3f(v, 0.0f, km1); }
+
+// T0 ~ N(setpoint, sigma) for (episode, global agent id): Box-Muller on one Philox block
+// (HPHeating.reset heating.py:145-152 with a counter-based stream; oracle/philox.py t0_draws)
+__device__ __forceinline__ void t0_draw(uint32_t k0, uint32_t k1, int episode, uint32_t gid, float setpoint,
+                                        double sigma, float& t_in, float& t_m) {
+  uint32_t c0 = 0, c1 = (uint32_t)episode, c2 = gid, c3 = kTagT0;
+  philox4x32_10(c0, c1, c2, c3, k0, k1);
+  const double u1 = ((double)c0 + 0.5) / 4294967296.0;
+  const double u2 = ((double)c1 + 0.5) / 4294967296.0;
+  const double rad = sqrt(-2.0 * log(u1));
+  const double ang = 6.283185307179586 * u2;
+  t_in = (float)((double)setpoint + sigma * (rad * cos(ang)));
+  t_m = (float)((double)setpoint + sigma * (rad * sin(ang)));
+}
+// Step pre-pass: everything of step t that depends only on the inputs (profiles, environment,
+// max_in), not on the policy or the temperatures, for every (t, agent) in one parallel launch per
+// episode, so the serial episode loop pays for none of these divisions and bins:
+//   pre[t][a].x = bits of balw = ((load - pv) / max_in) * max_in      agent.py:172-176, 210
+//   pre[t][a].y = (it_t * nT*nb + ib_t) | (it_{t+1} * nT*nb + ib_{t+1}) << 16
+//                 (row / np of the state (it, 0, ib, 0) and of the next state, rl.py:89-95;
+//                  the next state's balance is that of the next profile row, wrapping at T)
+// PHILOX = true also writes the step's exploration code words (philox_codes_kernel's job).
+__device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOut& o, size_t k) {
+  const int t = (int)(k / p.A), a = (int)(k % p.A);
+  const int tn = t + 1 == p.T ? 0 : t + 1;
+  const int se = p.n_env == 1 ? 0 : a / p.N;
+  const float mi = p.max_in[a];
+  const float2 f = p.prof[k], fn = p.prof[(size_t)tn * p.A + a];
+  const float bal = (f.x - f.y) / mi, baln = (fn.x - fn.y) / mi;
+  const float time_t = p.env[((size_t)t * p.n_env + se) * kEnvStride];
+  const float time_n = p.env[((size_t)tn * p.n_env + se) * kEnvStride];
+  const uint32_t tb = (uint32_t)(p.nT * p.nb);
+  const uint32_t lo = (uint32_t)idx_time(time_t, p.nt) * tb + (uint32_t)idx_plain(bal, p.nb);
+  const uint32_t hi = (uint32_t)idx_time(time_n, p.nt) * tb + (uint32_t)idx_plain(baln, p.nb);
+  o.pre[k] = make_uint2(__float_as_uint(bal * mi), lo | (hi << 16));
+  if (o.ipc) {
+    // N = 2: round 1's p2p feature depends only on the partner's round-0 action b (agent.py:203):
+    // its column entry is ev_b = ((balw_p + hp_p[b]) * 1) / 2 (the even split of round 0), summed
+    // as in the kernel's acc loop.  Byte b = the bin for b, so the kernel's round-1 rows can be
+    // issued a step ahead and picked by the partner's action.
+    const int i = a % 2, ap = a ^ 1;
+    const float2 fp = p.prof[(size_t)t * p.A + ap];
+    const float mip = p.max_in[ap];
+    const float balw_p = ((fp.x - fp.y) / mip) * mip;
+    const float4 lvp = p.hp_lv[ap];
+    const float hpl[3] = {lvp.x, lvp.y, lvp.z};
+    uint32_t ipc = 0;
+    for (int b = 0; b < 3; ++b) {
+      const float ev = div_n<2>((balw_p + hpl[b]) * 1.0f);
+      float acc = 0.0f;
+      for (int j = 0; j < 2; ++j) acc = acc + (-((j == i) ? 0.0f : ev));
+      ipc |= (uint32_t)idx_plain(div_n<2>(acc) / mi, p.np) << (8 * b);
+    }
+    o.ipc[k] = ipc;
+  }
+  if (o.words) {
+    EpisodeParams q = p;
+    q.episode = o.episode;
+    const int R1 = p.R + 1, W = (R1 + 3) >> 2;
+    for (int w = 0; w < W; ++w) {
+      uint32_t word = 0xFFFFFFFFu;
+      for (int b = 0; b < 4 && 4 * w + b < R1; ++b) {
+        const uint32_t c = philox_code(q, t, 4 * w + b, p.agent_offset + (uint32_t)a);
+        word = (word & ~(0xFFu << (8 * b))) | (c << (8 * b));
+      }
+      o.words[((size_t)t * W + w) * p.A + a] = word;
+    }
+  }
+}
+__global__ void step_prepass_kernel(const EpisodeParams p, const PrepOut o) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
+  if (k >= (size_t)p.T * p.A) return;
+  prepass_one(p, o, k);
+}
+
+// round 1 after an all-even round 0: every lane's row is ev (agent.py:190-191), so the column is
+// the group's ev values (one shuffle per partner instead of a row exchange)
+template <int N, int D, int G>
+__device__ __forceinline__ void gather_even(float ev, float (&col)[N], int i) {
+  if constexpr (D < G) {
+    const float got = shfl_xor_c<D>(ev);
+    const int src = i ^ D;
+#pragma unroll
+    for (int k = 0; k < N; ++k) col[k] = (k == src) ? got : col[k];
+    gather_even<N, D + 1, G>(ev, col, i);
+  }
+}
+
+// episode_fast_kernel: episode_kernel's per-agent-table path (no battery, no shared table,
+// G <= 8, R + 1 <= 4, code words from a pre-pass) with the rounds unrolled at compile time and the
+// policy-independent per-step work (balance, time / balance bins, the next state's bins) read
+// from step_prepass_kernel's output.  Same op order, same results, bit for bit (tests compare
+// both kernels with the oracle).  Latency structure per step:
+//   * round 0 always sees P = 0: its row and the next-state row are issued at the end of the
+//     previous step (as in episode_kernel), round 0 is an even split, and round 1's column is
+//     the group's round-0 even values;
+//   * the next step's pre-pass word, env row and code word are issued right after the dependent
+//     round-R gather, so waiting for that gather never waits for them (vmcnt counts in order);
+//   * every store is unconditional (inactive lanes and disabled records write a per-lane dummy
+//     slot), so the number of memory ops behind each load is static and the loop-top wait for
+//     the prefetched rows is vmcnt(3), not a vmcnt(0) drain of the step's stores;
+//   * records go out as ONE 32-B row per agent-step (FastRec) and are unpacked on request;
+//   * division by max_in / 60 / N uses the hoisted reciprocal (fdiv above).
+// spw = scenarios per wave (<= 64 / G): fewer scenarios per wave spread the waves over more CUs.
+struct FastRec {         // [T][A], 32 B
+  float reward, cost, grid, p2p, tin;
+  uint32_t actions;      // byte r: action of round r
+  uint32_t bins;         // (it * nT*nb + ib) | iT << 16
+  uint32_t ips;          // byte r: p2p bin of round r
+};
+template <int N, typename QT, int R1, bool TRAIN>
+__global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams p, const uint2* __restrict__ pre,
+                                                             FastRec* __restrict__ recs, int spw, int n_cons,
+                                                             const PrepOut nxt) {
+  // Blocks past the consumer grid are producers: the next episode's step pre-pass (speculating the
+  // same epsilon), run beside this episode's latency-bound waves on otherwise idle SIMDs, so the
+  // next launch needs neither a pre-pass launch nor a cross-stream wait.
+  if ((int)blockIdx.x >= n_cons) {
+    const size_t n = (size_t)p.T * p.A, stride = (size_t)(gridDim.x - n_cons) * kWave;
+    for (size_t k2 = (size_t)(blockIdx.x - n_cons) * kWave + threadIdx.x; k2 < n; k2 += stride) prepass_one(p, nxt, k2);
+    return;
+  }
+  constexpr int G = pow2ceil(N);
+  static_assert(G <= 8 && R1 >= 1 && R1 <= 4, "fast path: G <= 8, R + 1 <= 4");
+  // N = 2: round 1's Q row is one of three (by the partner's round-0 action) whose bins the
+  // pre-pass wrote; all three are issued a step ahead, so round 1 waits for no gather
+  constexpr bool CAND = N == 2 && R1 >= 2;
+  const int lane = (int)threadIdx.x;
+  const int sl = lane / G;
+  const int i = lane % G;
+  const int s = (int)blockIdx.x * spw + sl;
+  const bool active = i < N && sl < spw && s < p.S;
+  const int a = active ? s * N + i : 0;
+  const int s_env = p.n_env == 1 ? 0 : (active ? s : 0);
+  const int T = p.T;
+  const size_t A = (size_t)p.A;
+  const KC k = pin_constants(p);
+  const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
+  QT* __restrict__ q = reinterpret_cast<QT*>(p.q) + (size_t)a * n_states * kQPad;
+  const int np = k.np;
+  const int nbv = k.nb;
+  const float km1_T = (float)(k.nT - 1), km2_T = (float)(k.nT - 2), km1_p = (float)(np - 1), kp = (float)np;
+  const float mi = active ? p.max_in[a] : 1.0f;
+  const Recip rmi = recip(mi), rmph = recip(k.mph), rmargin = recip(k.margin), rn = recip((float)N);
+  const bool margin_one = p.margin == 1.0f;
+  const float4 lv = p.hp_lv[a];
+  float tin = active ? p.t_in[a] : k.setpoint;
+  float tm = active ? p.t_m[a] : k.setpoint;
+  const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, np);  // round 0 and next state: p2p = 0 (agent.py:203)
+  // stores of inactive lanes (and every record when none is requested) go to a per-lane dummy slot
+  QT* const q_dummy = reinterpret_cast<QT*>(p.dummy) + lane * kQPad;
+  FastRec* const rec_dummy = reinterpret_cast<FastRec*>(p.dummy) + kWave + lane;
+  const bool rec_on = p.record != 0 && active;
+  FastRec* rec_ptr = rec_on ? recs + a : rec_dummy;
+  const size_t rec_step = rec_on ? A : 0;
+
+  auto temp_bin = [&](float t_in) {  // idx_temp((T_in - setpoint) / margin) heating.py:118-120, rl.py:93
+    const float dt = t_in - k.setpoint;
+    const float x = margin_one ? dt : fdiv_b(dt, rmargin);
+    return clamp_bin_f(((x + 1.0f) / 2.0f) * km2_T + 1.0f, km1_T);
+  };
+  auto p2p_bin = [&](float x) { return clamp_bin_f(((x + 1.0f) / 2.0f) * kp, km1_p); };
+
+  const float* envb = p.env + (size_t)s_env * kEnvStride;
+  const size_t env_step = (size_t)p.n_env * kEnvStride;
+  const uint2* preb = pre + a;
+  const uint32_t* codes_a = p.codes + a;
+  const uint32_t* ipc_a = p.pre_ipc + a;  // read only when CAND
+  const int t1 = T > 1 ? 1 : 0;
+  // running (uniform, 32-bit) offsets of step t + 2, wrapping at T: T * A < 2^32 on this path
+  const uint32_t TA = (uint32_t)T * (uint32_t)A, env_st = (uint32_t)env_step, env_end = env_st * (uint32_t)T;
+  uint32_t o2 = (uint32_t)(2 % T) * (uint32_t)A, eo2 = (uint32_t)(2 % T) * env_st;
+
+  EnvRow e0 = load_env(envb);
+  EnvRow e1 = load_env(envb + (size_t)t1 * env_step);
+  uint2 p0 = preb[0];
+  uint2 p1 = preb[(size_t)t1 * A];
+  const uint32_t c0 = codes_a[0];
+  uint32_t c1 = codes_a[(size_t)t1 * A];
+  auto code_of = [&](uint32_t w) { return (TRAIN && active) ? w : 0xFFFFFFFFu; };
+  uint32_t cw = code_of(c0);
+  int iT = temp_bin(tin);
+  // row arithmetic in 24-bit multiplies (full-rate v_mul_u32_u24; every operand < 2^24)
+  auto strip_of = [&](uint32_t base, int it_) { return __umul24(base + __umul24((uint32_t)it_, (uint32_t)nbv), (uint32_t)np); };
+  uint32_t strip = strip_of(p0.y & 0xFFFFu, iT);
+  uint32_t nrow = strip_of(p0.y >> 16, iT) + (uint32_t)ip_zero;
+  auto row0_addr = [&](uint32_t st, uint32_t nr, uint32_t c) -> uint32_t {
+    const bool need = ((c & 0xFF) == 255) || (TRAIN && R1 == 1);  // greedy, or the TD target itself
+    return need ? st + (uint32_t)ip_zero : nr;
+  };
+  uint32_t a0 = row0_addr(strip, nrow, cw);
+  uint32_t aN = TRAIN ? nrow : a0;
+  Row4<QT> row0 = gather_row(q + a0 * kQPad);
+  Row4<QT> rowN = gather_row(q + aN * kQPad);
+  uint32_t ipc0 = 0, ipc1 = 0;
+  Row4<QT> cand[3];
+  if constexpr (CAND) {
+    ipc0 = ipc_a[0];
+    ipc1 = ipc_a[(size_t)t1 * A];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) cand[b] = gather_row(q + (strip + ((ipc0 >> (8 * b)) & 0xFFu)) * kQPad);
+  }
+  Patch<QT> pat{0xFFFFFFFFu, 0, (QT)0};
+  float ep_sum = 0.0f;
+  __builtin_amdgcn_s_waitcnt(0);  // enter the loop with nothing in flight (static waits inside)
+
+#pragma unroll 2
+  for (int t = 0; t < T; ++t) {
+    const float balw = __uint_as_float(p0.x);
+    float row[N];
+    float col[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) { row[j] = 0.0f; col[j] = 0.0f; }
+    row0 = patched(row0, a0, pat);  // the previous step's TD store may have hit a prefetched row
+    rowN = patched(rowN, aN, pat);
+
+    // round 0 (P = 0: every filtered power is -0, tot = 0, even split)
+    int code = (int)(cw & 0xFF);
+    int act = code == 255 ? argmax3(row0) : code;
+    float hp = hp_of(lv, act);
+    int ip = ip_zero;
+    Row4<QT> rowR = row0;
+    uint32_t acts = (uint32_t)act, ips = (uint32_t)ip_zero;
+    const float ev0 = div_n_r<N>((balw + hp) * 1.0f, rn);
+#pragma unroll
+    for (int j = 0; j < N; ++j) row[j] = ev0;
+    EnvRow e2;
+    uint2 p2;
+    uint32_t c2, ipc2 = 0;
+    if constexpr (CAND) {  // no round-1 gather to hide behind: issue the step t + 2 inputs now
+      e2 = load_env(envb + eo2);
+      p2 = preb[o2];
+      c2 = codes_a[o2];
+      ipc2 = ipc_a[o2];
+    }
+#pragma unroll
+    for (int r = 1; r < R1; ++r) {
+      if (r == 1) {
+        gather_even<N, 1, G>(ev0, col, i);
+      } else {
+        exchange<N>(row, col, i, sl, nullptr);
+      }
+      code = (int)((cw >> (8 * r)) & 0xFF);
+      if (CAND && r == 1) {
+        // the partner's round-0 action picks the prefetched row (its bin is byte b of ipc0)
+        const int b = __float_as_int(shfl_xor_c<1>(__int_as_float(act)));
+        ip = (int)((ipc0 >> (8 * b)) & 0xFFu);
+        rowR = patched(sel_row(b, cand[0], cand[1], cand[2]), strip + (uint32_t)ip, pat);
+      } else {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : col[j]));
+        ip = p2p_bin(fdiv_b(div_n_r<N>(acc, rn), rmi));
+        const bool need = code == 255 || (TRAIN && r == R1 - 1);
+#if P2PMG_ABLATE == 7
+        rowR = fake_row(q + (need ? strip + (uint32_t)ip : a0) * kQPad);
+#else
+        rowR = gather_row(q + (need ? strip + (uint32_t)ip : a0) * kQPad);
+#endif
+      }
+      if (!CAND && r == R1 - 1) {  // next inputs, issued behind the dependent gather
+        e2 = load_env(envb + eo2);
+        p2 = preb[o2];
+        c2 = codes_a[o2];
+      }
+      act = code == 255 ? argmax3(rowR) : code;
+      acts |= (uint32_t)act << (8 * r);
+      ips |= (uint32_t)ip << (8 * r);
+      hp = hp_of(lv, act);
+      const float out = balw + hp;
+      // _divide_power's filter keeps pw where sign(out) != sign(pw) (agent.py:187-188): for out > 0
+      // that is pw <= 0, for out < 0 pw >= 0, for out = 0 any pw.  A kept pw = +-0 and a dropped
+      // one (0) are interchangeable: every later use is |f| or a sum that already holds +0.
+      // As one clamp: f = med3(pw, out < 0 ? 0 : -inf, out > 0 ? 0 : +inf).
+      const float flo = out < 0.0f ? 0.0f : -__builtin_inff(), fhi = out > 0.0f ? 0.0f : __builtin_inff();
+      float f[N];
+      float tot = 0.0f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const float pw = -((j == i) ? 0.0f : col[j]);
+        f[j] = __builtin_amdgcn_fmed3f(pw, flo, fhi);
+        tot = tot + f[j];
+      }
+      tot = fabsf(tot);
+      const float ev = div_n_r<N>(out * 1.0f, rn);
+      // out * |f_j| / tot for every j: the diagonal's f_ii = +-0 gives out * 0 / tot = out * 0, the
+      // reference's value for it (agent.py:193-194), for any tot > 0.  One range guard per round.
+      const Recip rt = recip(tot == 0.0f ? 1.0f : tot);  // the tot = 0 lanes take ev
+      float num[N];
+      bool bad = !rt.ok;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        num[j] = out * fabsf(f[j]);
+        row[j] = fdiv_core(num[j], rt);
+        bad = bad || !fdiv_ok(num[j]);
+      }
+      if (bad) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) row[j] = fdiv_ieee(num[j], rt.b);
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) row[j] = (tot == 0.0f) ? ev : row[j];
+    }
+    if constexpr (R1 == 1) {
+      e2 = load_env(envb + eo2);
+      p2 = preb[o2];
+      c2 = codes_a[o2];
+    }
+
+    // CommunityMicrogrid._step -> HPHeating.step (community.py:184-188, heating.py:138-143), then
+    // the next step's rows are issued before this step's market work
+    float tin1 = tin, tm1 = tm;
+    rc_update(k, e0.t_out, hp, tin1, tm1);
+    const int iT1 = temp_bin(tin1);
+    const uint32_t strip1 = strip_of(p1.y & 0xFFFFu, iT1);
+    const uint32_t nrow1 = strip_of(p1.y >> 16, iT1) + (uint32_t)ip_zero;
+    const uint32_t cw1 = code_of(c1);
+    const uint32_t a0n = row0_addr(strip1, nrow1, cw1);
+    const uint32_t aNn = TRAIN ? nrow1 : a0n;
+#if P2PMG_ABLATE == 8
+    const Row4<QT> row0n = fake_row(q + a0n * kQPad);
+    const Row4<QT> rowNn = fake_row(q + aNn * kQPad);
+#else
+    const Row4<QT> row0n = gather_row(q + a0n * kQPad);
+    const Row4<QT> rowNn = gather_row(q + aNn * kQPad);
+#endif
+    Row4<QT> candn[3];
+    if constexpr (CAND) {
+#pragma unroll
+      for (int b = 0; b < 3; ++b) candn[b] = gather_row(q + (strip1 + ((ipc1 >> (8 * b)) & 0xFFu)) * kQPad);
+    }
+    pat.row = 0xFFFFFFFFu;
+
+    // CommunityMicrogrid._assign_powers community.py:45-54 on the final P (diagonal kept)
+    exchange<N>(row, col, i, sl, nullptr);
+    float g = 0.0f, pp = 0.0f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      // ex = sign(pij) * min(|pij|, |pji|) where the signs differ (community.py:48-50).  With a
+      // zero operand min(...) = 0, so ex = +-0 and g, pp (which start at +0) take the same values
+      // as with the reference's 0; otherwise "signs differ" is "sign bits differ".
+      const float pij = row[j], pji = col[j];
+      const float mn = __builtin_amdgcn_fmed3f(fabsf(pij), fabsf(pji), -__builtin_inff());  // min of the two
+      const bool opp = ((__float_as_uint(pij) ^ __float_as_uint(pji)) >> 31) != 0u;
+      const float ex = opp ? __builtin_copysignf(mn, pij) : 0.0f;
+      g = g + (pij - ex);
+      pp = pp + ex;
+    }
+    // CommunityMicrogrid._compute_costs community.py:56-65
+    float cost = (g >= 0.0f) ? g * e0.buy : g * e0.inj;
+    cost = cost + pp * e0.p2p;
+    cost = fdiv_b(cost * k.slot, rmph);
+    cost = cost * k.kilo;
+    // RLAgent.get_reward agent.py:225-232 (pre-update T_in)
+    float pen = fmaxf(fmaxf(0.0f, k.lower - tin), fmaxf(0.0f, tin - k.upper));
+    pen = pen > 0.0f ? pen + 1.0f : 0.0f;
+    const float rw = -(cost + k.penw * pen);
+
+    if constexpr (TRAIN) {
+      // QAgent.train agent.py:293-298 -> QActor.train rl.py:119-129
+      const uint32_t srow = strip + (uint32_t)ip;
+      const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
+      const QT qnew = td_update(qsa, rw, max3(rowN), k.alpha, k.gamma);
+      *(active ? q + srow * kQPad + act : q_dummy) = qnew;
+      pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
+    }
+    {
+      const uint32_t bins = (p0.y & 0xFFFFu) | ((uint32_t)iT << 16);  // it * nT*nb + ib | iT << 16
+      float4* rp = reinterpret_cast<float4*>(rec_ptr);
+      rp[0] = make_float4(rw, cost, g, pp);
+      rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
+      rec_ptr += rec_step;
+    }
+    // avg_reward = sum_t mean_i r (community.py:179), canonical sequential order
+    const float m = group_sum<N>(rw, lane, i, sl, nullptr);
+    ep_sum = ep_sum + div_n_r<N>(m, rn);
+
+    tin = tin1;
+    tm = tm1;
+    iT = iT1;
+    e0 = e1;
+    e1 = e2;
+    p0 = p1;
+    p1 = p2;
+    c1 = c2;
+    o2 += (uint32_t)A;
+    o2 = o2 == TA ? 0u : o2;
+    eo2 += env_st;
+    eo2 = eo2 == env_end ? 0u : eo2;
+    strip = strip1;
+    cw = cw1;
+    a0 = a0n;
+    aN = aNn;
+    row0 = row0n;
+    rowN = rowNn;
+    if constexpr (CAND) {
+      ipc0 = ipc1;
+      ipc1 = ipc2;
+#pragma unroll
+      for (int b = 0; b < 3; ++b) cand[b] = candn[b];
+    }
+  }
+  if (active) {
+    if (p.reset_t0)  // agent.reset() at the end of train_episode (community.py:181), fused
+      t0_draw(p.seed_lo, p.seed_hi, p.episode + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, tin, tm);
+    p.t_in[a] = tin;
+    p.t_m[a] = tm;
+    if (i == 0) p.ep_reward[s] = ep_sum;
+  }
+}
+
+// FastRec rows -> the general record buffers (reward, cost, grid, p2p, tin [T][A]; action u8 and
+// packed index i32 [T][R+1][A]), for the records the caller asks for
+__global__ void fast_rec_unpack_kernel(int T, int R1, int A, uint32_t tb, const FastRec* __restrict__ recs, int which,
+                                       void* __restrict__ out) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
+  if (k >= (size_t)T * A) return;
+  const FastRec r = recs[k];
+  if (which < 5) {
+    const float v[5] = {r.reward, r.cost, r.grid, r.p2p, r.tin};
+    reinterpret_cast<float*>(out)[k] = v[which];
+    return;
+  }
+  const size_t t = k / A, a = k % A;
+  for (int rr = 0; rr < R1; ++rr) {
+    const size_t kk = (t * R1 + rr) * A + a;
+    if (which == 5)
+      reinterpret_cast<uint8_t*>(out)[kk] = (uint8_t)(r.actions >> (8 * rr));
+    else
+      reinterpret_cast<int32_t*>(out)[kk] = (int32_t)(((r.bins & 0xFFFFu) / tb) | ((r.bins >> 16) << 8) |
+                                                      (((r.bins & 0xFFFFu) % tb) << 16) | (((r.ips >> (8 * rr)) & 0xFFu) << 24));
+  }
+}
+
+// hipExtLaunchKernel stamps the start / stop events from the dispatch itself: no marker packets
+// between back-to-back episodes
+template <int N, typename QT, int R1>
+void launch_fast_r(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
+                   const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  if (p.mode == 0)
+    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, true>), dim3(blocks + prod), dim3(kWave), 0, st, ev0, ev1, 0,
+                          p, pre, recs, spw, blocks, nxt);
+  else
+    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, false>), dim3(blocks + prod), dim3(kWave), 0, st, ev0, ev1,
+                          0, p, pre, recs, spw, blocks, nxt);
+}
+
+template <int N, typename QT>
+hipError_t launch_fast_n(const EpisodeParams& p, const uint2* pre, void* recs, int spw, const PrepOut* nxt,
+                         hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  constexpr int G = pow2ceil(N);
+  if (spw <= 0 || spw > kWave / G) spw = kWave / G;
+  const int blocks = (p.S + spw - 1) / spw;
+  const size_t n = (size_t)p.T * p.A;
+  const int prod = nxt ? (int)std::min<size_t>(2048, (n + kWave - 1) / kWave) : 0;
+  const PrepOut none{nullptr, nullptr, nullptr, 0};
+  FastRec* r = reinterpret_cast<FastRec*>(recs);
+  switch (p.R + 1) {
+    case 1: launch_fast_r<N, QT, 1>(p, pre, r, blocks, spw, prod, nxt ? *nxt : none, ev0, ev1, st); break;
+    case 2: launch_fast_r<N, QT, 2>(p, pre, r, blocks, spw, prod, nxt ? *nxt : none, ev0, ev1, st); break;
+    case 3: launch_fast_r<N, QT, 3>(p, pre, r, blocks, spw, prod, nxt ? *nxt : none, ev0, ev1, st); break;
+    case 4: launch_fast_r<N, QT, 4>(p, pre, r, blocks, spw, prod, nxt ? *nxt : none, ev0, ev1, st); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <typename QT>
+hipError_t launch_fast_q(const EpisodeParams& p, const uint2* pre, void* recs, int spw, const PrepOut* nxt,
+                         hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  switch (p.N) {
+    case 1: return launch_fast_n<1, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
+    case 2: return launch_fast_n<2, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
+    case 3: return launch_fast_n<3, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
+    case 4: return launch_fast_n<4, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
+    case 5: return launch_fast_n<5, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
+    case 6: return launch_fast_n<6, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
+    case 7: return launch_fast_n<7, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
+    case 8: return launch_fast_n<8, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 template <int N, typename QT, bool SQ>
 void launch_nq(const EpisodeParams& p, hipStream_t st) {
   constexpr int SPW = kWave / pow2ceil(N);
@@ -775,14 +1333,7 @@ __global__ void t0_philox_kernel(int A, float* t_in, float* t_m, uint32_t k0, ui
                                  uint32_t agent_offset, float setpoint, double sigma) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= A) return;
-  uint32_t c0 = 0, c1 = (uint32_t)episode, c2 = agent_offset + (uint32_t)k, c3 = kTagT0;
-  philox4x32_10(c0, c1, c2, c3, k0, k1);
-  const double u1 = ((double)c0 + 0.5) / 4294967296.0;
-  const double u2 = ((double)c1 + 0.5) / 4294967296.0;
-  const double rad = sqrt(-2.0 * log(u1));
-  const double ang = 6.283185307179586 * u2;
-  t_in[k] = (float)((double)setpoint + sigma * (rad * cos(ang)));
-  t_m[k] = (float)((double)setpoint + sigma * (rad * sin(ang)));
+  t0_draw(k0, k1, episode, agent_offset + (uint32_t)k, setpoint, sigma, t_in[k], t_m[k]);
 }
 
 // reference layout [count][n_states][n_actions] (host dtype) <-> padded device layout
@@ -868,6 +1419,28 @@ hipError_t launch_battery_seq(int agents, int steps, const double* bal, double* 
   if (agents <= 0) return hipSuccess;
   hipLaunchKernelGGL(battery_seq_kernel, dim3(grid_for(agents, 64)), dim3(64), 0, stream, agents, steps, bal, out_bal,
                      soc_hist, soc, cap, smin, smax, sqrt_eff);
+  return hipGetLastError();
+}
+
+hipError_t launch_step_prepass(const EpisodeParams& p, const PrepOut& o, hipStream_t stream) {
+  const size_t n = (size_t)p.T * p.A;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(step_prepass_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, p, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_episode_fast(const EpisodeParams& p, const uint2* pre, void* recs, int q_dtype, int spw,
+                               const PrepOut* next, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream) {
+  return q_dtype == 0 ? launch_fast_q<double>(p, pre, recs, spw, next, ev0, ev1, stream)
+                      : launch_fast_q<float>(p, pre, recs, spw, next, ev0, ev1, stream);
+}
+
+hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void* recs, int which, void* out,
+                                  hipStream_t stream) {
+  const size_t n = (size_t)T * A;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(fast_rec_unpack_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, T, R1, A, tb,
+                     reinterpret_cast<const FastRec*>(recs), which, out);
   return hipGetLastError();
 }
 

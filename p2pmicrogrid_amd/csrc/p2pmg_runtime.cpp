@@ -6,10 +6,12 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -25,6 +27,7 @@ struct p2pmg_ctx {
   p2pmg_config cfg{};
   int device = 0;
   int S = 0, N = 0, R = 0, T = 0, A = 0;
+  int n_cu = 256;  // compute units of the device (multiProcessorCount)
   size_t n_states = 0;
   size_t q_elem = 8;
   hipStream_t stream = nullptr;
@@ -42,6 +45,22 @@ struct p2pmg_ctx {
   float* t_m = nullptr;
   void* q = nullptr;
   uint32_t* codes = nullptr;  // code words [T][W][A]
+  // fast path: step pre-pass outputs, double-buffered.  Episode e's launch also computes, in extra
+  // workgroups, slot (e+1)'s pre-pass for episode e + 1 at the same epsilon (it reads only inputs,
+  // never Q or T); run_episode(e + 1) uses it when its arguments match (spec_*), else recomputes.
+  uint2* pre[2] = {nullptr, nullptr};        // [T][A] {balw, bins}
+  uint32_t* pre_ipc[2] = {nullptr, nullptr}; // N = 2: [T][A] round-1 bins per partner action
+  uint32_t* pcodes[2] = {nullptr, nullptr};  // Philox code words [T][W][A]
+  int pslot = 0;
+  bool spec_valid[2] = {false, false};
+  int spec_episode[2] = {0, 0};
+  double spec_eps[2] = {0.0, 0.0};
+  long long spec_version[2] = {-1, -1};
+  long long inputs_version = 0;  // bumped by every input upload (env, profiles, max_in, hp levels)
+  bool mi_ok = false;         // every max_in inside the fast division range (fdiv in p2pmg_kernels.hip)
+  void* dummy = nullptr;      // fast path: target of masked-off stores (2 * 64 * 32 B)
+  void* rec_pack = nullptr;   // fast path: packed records [T][A] x 32 B
+  int rec_fast_mask = 0;      // records of the last episode that live (packed) in rec_pack
   int code_src = 0;          // what the code buffer holds: 0 none, 1 replay upload, 2 Philox pre-pass
   float* ep_reward = nullptr;
   float* rec_f32[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // reward, cost, grid, p2p, tin
@@ -239,6 +258,8 @@ int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
   };
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return bail(P2PMG_E_HIP);
+  hipDeviceProp_t prop{};
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->n_cu = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(P2PMG_E_HIP);
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) return bail(P2PMG_E_HIP);
   const size_t A = (size_t)c->A;
@@ -250,6 +271,7 @@ int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
   // kernel's code loads unconditional
   const size_t ncw = (size_t)c->T * ((c->R + 4) / 4) * A;
   if (dmalloc(&c->codes, ncw) != hipSuccess) return bail(P2PMG_E_NOMEM);
+  if (hipMalloc(&c->dummy, 2 * 64 * p2pmg::kFastRecBytes) != hipSuccess) return bail(P2PMG_E_NOMEM);
   if (hipMemsetAsync(c->codes, 0xFF, ncw * 4, c->stream) != hipSuccess) return bail(P2PMG_E_HIP);
   if (cfg->learner != P2PMG_LEARNER_TABULAR && cfg->learner != P2PMG_LEARNER_DQN) return bail(P2PMG_E_INVALID);
   c->dqn = cfg->learner == P2PMG_LEARNER_DQN;
@@ -290,6 +312,13 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   dfree(c->t_m);
   if (c->q) (void)hipFree(c->q);
   dfree(c->codes);
+  for (int k = 0; k < 2; ++k) {
+    dfree(c->pre[k]);
+    dfree(c->pre_ipc[k]);
+    dfree(c->pcodes[k]);
+  }
+  if (c->dummy) (void)hipFree(c->dummy);
+  if (c->rec_pack) (void)hipFree(c->rec_pack);
   dfree(c->ep_reward);
   for (auto& b : c->rec_f32) dfree(b);
   dfree(c->rec_action);
@@ -341,6 +370,7 @@ int p2pmg_device_info(p2pmg_ctx* c, char* name, size_t name_len, size_t* total_m
 
 int p2pmg_set_env(p2pmg_ctx* c, int n_env, const float* time, const float* t_out, const float* buy, const float* inj,
                   const float* p2p) {
+  if (c) c->inputs_version++;  // invalidates the speculative pre-pass slots
   if (!c || !time || !t_out || !buy || !inj || !p2p) return P2PMG_E_INVALID;
   if (n_env != 1 && n_env != c->S) return fail(c, P2PMG_E_INVALID, "n_env must be 1 or S");
   const size_t T = c->T;
@@ -367,6 +397,7 @@ int p2pmg_set_env(p2pmg_ctx* c, int n_env, const float* time, const float* t_out
 }
 
 int p2pmg_set_profiles(p2pmg_ctx* c, const float* load_w, const float* pv_w) {
+  if (c) c->inputs_version++;  // invalidates the speculative pre-pass slots
   if (!c || !load_w || !pv_w) return P2PMG_E_INVALID;
   const size_t n = (size_t)c->A * c->T;
   float *dl = nullptr, *dp = nullptr;
@@ -388,9 +419,15 @@ int p2pmg_set_profiles(p2pmg_ctx* c, const float* load_w, const float* pv_w) {
 }
 
 int p2pmg_set_agent_params(p2pmg_ctx* c, const float* max_in) {
+  if (c) c->inputs_version++;  // invalidates the speculative pre-pass slots
   if (!c || !max_in) return P2PMG_E_INVALID;
   HIP_TRY(c, hipMemcpyAsync(c->max_in, max_in, (size_t)c->A * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->mi_ok = true;
+  for (int a = 0; a < c->A; ++a) {
+    const float m = std::fabs(max_in[a]);
+    if (!(m >= 0x1p-40f && m <= 0x1p40f)) c->mi_ok = false;
+  }
   c->have_params = true;
   return P2PMG_OK;
 }
@@ -531,6 +568,7 @@ static EpisodeParams episode_params(p2pmg_ctx* c, const p2pmg_episode_args* args
   p.bat_max = c->bat_max;
   p.bat_sqrt_eff = c->bat_sqrt_eff;
   p.hp_lv = c->hp_lv;
+  p.dummy = c->dummy;
   p.nt = g.n_time_states;
   p.nT = g.n_temp_states;
   p.nb = g.n_balance_states;
@@ -561,6 +599,12 @@ static EpisodeParams episode_params(p2pmg_ctx* c, const p2pmg_episode_args* args
 
 static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args);
 
+// divisors the fast kernel divides by with the range-free quotient (fdiv_b in p2pmg_kernels.hip)
+static bool host_div_range(float b) {
+  const float m = std::fabs(b);
+  return m >= 0x1p-40f && m <= 0x1p40f;
+}
+
 int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   if (!c || !args) return P2PMG_E_INVALID;
   if (c->dqn) return dqn_run_episode(c, args);
@@ -575,7 +619,47 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   if (rc != P2PMG_OK) return rc;
   EpisodeParams p = episode_params(c, args);
   const p2pmg_config& g = c->cfg;
-  if (train && args->rng == P2PMG_RNG_PHILOX) {
+  // fast per-agent-table path (episode_fast_kernel): automatic whenever it applies
+  static const int env_spw = [] { const char* v = getenv("P2PMG_SPW"); return v ? atoi(v) : 0; }();
+  static const bool env_general = [] { const char* v = getenv("P2PMG_KERNEL"); return v && !strcmp(v, "general"); }();
+  const bool fast = !g.shared_q && !c->battery && c->N <= 8 && c->R + 1 <= 4 && c->mi_ok &&
+                    (long long)g.n_time_states * g.n_temp_states * g.n_balance_states < 65536 &&
+                    (long long)c->T * c->A < (1LL << 32) && host_div_range(g.minutes_per_hour) &&
+                    host_div_range(g.temp_margin) &&
+                    !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_PHILOX_INKERNEL)) && !env_general;
+  const int ps = c->pslot;
+  p2pmg::PrepOut next{};
+  bool produce = false;
+  if (fast) {
+    const size_t ta = (size_t)c->T * c->A;
+    const bool philox = train && args->rng == P2PMG_RNG_PHILOX;
+    const bool want_ipc = c->N == 2 && c->R >= 1;
+    for (int k = 0; k < 2; ++k) {  // both slots (the launch writes the other one)
+      if (!c->pre[k]) HIP_TRY(c, dmalloc(&c->pre[k], ta));
+      if (want_ipc && !c->pre_ipc[k]) HIP_TRY(c, dmalloc(&c->pre_ipc[k], ta));
+      if (philox && !c->pcodes[k]) HIP_TRY(c, dmalloc(&c->pcodes[k], ta * ((c->R + 4) / 4)));
+    }
+    p.pre_ipc = want_ipc ? c->pre_ipc[ps] : nullptr;
+    if (philox) p.codes = c->pcodes[ps];
+    p.rng = 0;
+    if (args->record && !c->rec_pack) HIP_TRY(c, hipMalloc(&c->rec_pack, ta * p2pmg::kFastRecBytes));
+    // this slot's pre-pass: computed by the previous launch if it guessed these arguments
+    const bool hit = c->spec_valid[ps] && c->spec_version[ps] == c->inputs_version &&
+                     (!philox || (c->spec_episode[ps] == args->episode && c->spec_eps[ps] == args->epsilon));
+    if (!hit) {
+      const p2pmg::PrepOut o{c->pre[ps], p.pre_ipc, philox ? c->pcodes[ps] : nullptr, args->episode};
+      HIP_TRY(c, p2pmg::launch_step_prepass(p, o, c->stream));
+    }
+    // the next slot, for episode + 1 at the same epsilon (Philox draws only when this one has them)
+    const int ns = ps ^ 1;
+    next = p2pmg::PrepOut{c->pre[ns], want_ipc ? c->pre_ipc[ns] : nullptr, philox ? c->pcodes[ns] : nullptr,
+                          args->episode + 1};
+    produce = true;
+    c->spec_valid[ns] = true;
+    c->spec_version[ns] = c->inputs_version;
+    c->spec_episode[ns] = philox ? args->episode + 1 : -1;
+    c->spec_eps[ns] = args->epsilon;
+  } else if (train && args->rng == P2PMG_RNG_PHILOX) {
     bool prepass = c->A < (1 << 18);
     if (args->flags & P2PMG_FLAG_PHILOX_PREPASS) prepass = true;
     if (args->flags & P2PMG_FLAG_PHILOX_INKERNEL) prepass = false;
@@ -595,12 +679,29 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   }
   const int slot = (int)(c->n_timed % p2pmg_ctx::kRing);
   hipEvent_t r0 = c->ring[2 * slot], r1 = c->ring[2 * slot + 1];
-  HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  HIP_TRY(c, hipEventRecord(r0, c->stream));
-  hipError_t e = p2pmg::launch_episode(p, g.q_dtype, c->stream);
+  if (!fast) HIP_TRY(c, hipEventRecord(r0, c->stream));
+  int spw = args->scen_per_wave > 0 ? args->scen_per_wave : env_spw;
+  if (spw <= 0) {  // automatic: full waves, or spread a small batch over all CUs (one wave per CU)
+    const int full = 64 / (c->N <= 1 ? 1 : c->N <= 2 ? 2 : c->N <= 4 ? 4 : 8);
+    const int waves = (c->S + full - 1) / full;
+    spw = waves >= c->n_cu ? full : std::max(full / 4, (c->S + c->n_cu - 1) / c->n_cu);
+    spw = std::min(spw, full);
+  }
+  const bool reset = (args->flags & P2PMG_FLAG_RESET_T0) != 0;
+  p.reset_t0 = (fast && reset) ? 1 : 0;
+  p.reset_sigma = args->reset_sigma;
+  hipError_t e = fast ? p2pmg::launch_episode_fast(p, c->pre[ps], c->rec_pack, g.q_dtype, spw,
+                                                  produce ? &next : nullptr, r0, r1, c->stream)
+                     : p2pmg::launch_episode(p, g.q_dtype, c->stream);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));
-  HIP_TRY(c, hipEventRecord(r1, c->stream));
-  HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
+  c->rec_fast_mask = fast ? (args->record & 127) : 0;
+  if (!fast) HIP_TRY(c, hipEventRecord(r1, c->stream));
+  if (fast) c->pslot ^= 1;
+  if (reset && !fast) {  // general kernel: the reset as its own launch
+    const uint32_t off = (uint32_t)(g.scenario_offset * c->N);
+    HIP_TRY(c, p2pmg::launch_t0_philox(c->A, c->t_in, c->t_m, p.seed_lo, p.seed_hi, args->episode + 1, off,
+                                       g.setpoint, args->reset_sigma, c->stream));
+  }
   c->timed = true;
   c->n_timed++;
   return P2PMG_OK;
@@ -608,9 +709,10 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
 
 int p2pmg_last_kernel_ms(p2pmg_ctx* c, float* ms) {
   if (!c || !ms) return P2PMG_E_INVALID;
-  if (!c->timed) return fail(c, P2PMG_E_STATE, "no episode launched yet");
-  HIP_TRY(c, hipEventSynchronize(c->ev1));
-  HIP_TRY(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+  if (!c->timed || c->n_timed == 0) return fail(c, P2PMG_E_STATE, "no episode launched yet");
+  const int slot = (int)((c->n_timed - 1) % p2pmg_ctx::kRing);  // the ring pair of the last launch
+  HIP_TRY(c, hipEventSynchronize(c->ring[2 * slot + 1]));
+  HIP_TRY(c, hipEventElapsedTime(ms, c->ring[2 * slot], c->ring[2 * slot + 1]));
   return P2PMG_OK;
 }
 
@@ -658,6 +760,11 @@ int p2pmg_get_record(p2pmg_ctx* c, int which, void* host) {
     return fail(c, P2PMG_E_INVALID, "get_record: unknown record");
   }
   if (!src) return fail(c, P2PMG_E_STATE, "get_record: record was never requested");
+  if (c->rec_fast_mask & which) {  // the last episode ran the fast kernel: unpack its rows
+    const int w = slot >= 0 ? slot : (which == P2PMG_REC_ACTION ? 5 : 6);
+    const uint32_t tb = (uint32_t)(c->cfg.n_temp_states * c->cfg.n_balance_states);
+    HIP_TRY(c, p2pmg::launch_fast_rec_unpack(c->T, c->R + 1, c->A, tb, c->rec_pack, w, const_cast<void*>(src), c->stream));
+  }
   HIP_TRY(c, hipMemcpyAsync(host, src, bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return P2PMG_OK;
@@ -716,6 +823,7 @@ int p2pmg_state_indices(p2pmg_ctx* c, int n, const float* obs, int32_t* idx) {
 }
 
 int p2pmg_set_hp_levels(p2pmg_ctx* c, const float* levels) {
+  if (c) c->inputs_version++;  // invalidates the speculative pre-pass slots
   if (!c || !levels) return P2PMG_E_INVALID;
   std::vector<float4> lv((size_t)c->A);
   for (size_t a = 0; a < lv.size(); ++a) lv[a] = make_float4(levels[3 * a], levels[3 * a + 1], levels[3 * a + 2], 0.0f);
@@ -1124,6 +1232,7 @@ static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d) {
 }
 
 static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
+  c->rec_fast_mask = 0;
   int rc = dqn_ready(c, "run_episode");
   if (rc != P2PMG_OK) return rc;
   const int mode = args->mode;
@@ -1149,7 +1258,6 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     for (auto& ev : c->ring) HIP_TRY(c, hipEventCreate(&ev));
   }
   const int slot = (int)(c->n_timed % p2pmg_ctx::kRing);
-  HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
   HIP_TRY(c, hipEventRecord(c->ring[2 * slot], c->stream));
   for (int t = 0; t < c->T; ++t) {
     d.t = t;
@@ -1161,7 +1269,6 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     }
   }
   HIP_TRY(c, hipEventRecord(c->ring[2 * slot + 1], c->stream));
-  HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
   c->n_timed++;
   if (acting) c->d_added_min += c->T;

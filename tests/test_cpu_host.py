@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_lib.EXPORTS)
-    assert L.p2pmg_abi_version() == 1
+    assert L.p2pmg_abi_version() == 2
 
 
 def test_config_default_matches_reference_constants():

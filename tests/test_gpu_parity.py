@@ -104,11 +104,16 @@ def _compare(out, rec, tag):
     assert np.array_equal(unpack_index(rec["index"]), out["idx"]), tag
 
 
-@pytest.mark.parametrize("N,R,T,q_dtype", [(2, 1, 96, "f64"), (3, 2, 48, "f64"), (5, 0, 40, "f64"),
-                                            (8, 1, 24, "f64"), (16, 1, 12, "f64"), (1, 1, 30, "f64"),
-                                            (2, 1, 96, "f32"), (4, 3, 20, "f32"), (2, 7, 10, "f64"),
-                                            (6, 4, 10, "f32")])
-def test_replay_batch_matches_oracle(N, R, T, q_dtype):
+CASES = [(2, 1, 96, "f64"), (3, 2, 48, "f64"), (5, 0, 40, "f64"), (8, 1, 24, "f64"), (16, 1, 12, "f64"),
+         (1, 1, 30, "f64"), (2, 1, 96, "f32"), (4, 3, 20, "f32"), (2, 7, 10, "f64"), (6, 4, 10, "f32"),
+         (7, 2, 16, "f64"), (3, 3, 12, "f32")]
+# kernel choice x scenarios per wave: the fast kernel (auto), partially filled fast waves, the general kernel
+KERNELS = [("auto", 0), ("auto", 5), ("general", 0)]
+
+
+@pytest.mark.parametrize("kernel,spw", KERNELS)
+@pytest.mark.parametrize("N,R,T,q_dtype", CASES)
+def test_replay_batch_matches_oracle(N, R, T, q_dtype, kernel, spw):
     """Many scenarios, each with its own RandomState(42 + s) replay stream, several episodes."""
     S = 64
     inp = scenario_batch(S, N, T, seed=7)
@@ -119,7 +124,7 @@ def test_replay_batch_matches_oracle(N, R, T, q_dtype):
     for e, eps in enumerate((0.81, 0.729, 0.2)):
         codes = np.stack([reference_replay_codes(rs, T, R, N, eps) for rs in rss], axis=2)  # [T,R+1,S,N]
         eng.set_replay_codes(codes)
-        eng.run_episode("train", "replay", episode=e, epsilon=eps, record=REC)
+        eng.run_episode("train", "replay", episode=e, epsilon=eps, record=REC, kernel=kernel, scen_per_wave=spw)
         out = ob.run_episode("train", codes=codes, eps=eps)
         _compare(out, eng.get_records(REC), (N, R, T, q_dtype, e))
         assert np.array_equal(eng.episode_reward(), out["episode_reward"])
@@ -128,7 +133,7 @@ def test_replay_batch_matches_oracle(N, R, T, q_dtype):
     q = eng.get_q(dtype=np.float64 if q_dtype == "f64" else np.float32)
     assert np.array_equal(q.reshape(S * N, -1, 3), ob.q)
     # greedy pass with the learned tables
-    eng.run_episode("greedy", record=REC)
+    eng.run_episode("greedy", record=REC, kernel=kernel, scen_per_wave=spw)
     _compare(ob.run_episode("greedy"), eng.get_records(REC), "greedy")
 
 
@@ -220,3 +225,42 @@ def test_q_roundtrip_and_sharded_offsets():
     for k in REC:
         ax = 2 if k in ("action", "index") else 1
         assert np.array_equal(np.concatenate([p[k] for p in parts], axis=ax), full[k]), k
+
+
+@pytest.mark.parametrize("kernel", ["auto", "general"])
+def test_unrecorded_episodes_match_oracle(kernel):
+    """No records requested (the fast kernel's stores all go to its dummy slots except the TD
+    updates): Q-tables, episode rewards and final temperatures still match the oracle."""
+    S, N, R, T = 96, 3, 1, 48
+    inp = scenario_batch(S, N, T, seed=21)
+    ob = _oracle_for(inp, N, R)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = _device_for(inp, N, R)
+    for e in range(3):
+        eng.run_episode("train", "philox", episode=e, epsilon=0.6, kernel=kernel)
+        out = ob.run_episode("train", rng="philox", seed=42, episode=e, eps=0.6)
+        assert np.array_equal(eng.episode_reward(), out["episode_reward"]), e
+        a, b = eng.get_temperatures()
+        assert np.array_equal(a, out["t_in_final"]) and np.array_equal(b, out["t_m_final"]), e
+    assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
+    eng.run_episode("greedy", kernel=kernel)
+    assert np.array_equal(eng.episode_reward(), ob.run_episode("greedy")["episode_reward"])
+
+
+@pytest.mark.parametrize("kernel", ["auto", "general"])
+def test_fused_t0_reset_equals_separate_reset(kernel):
+    """reset_sigma fuses agent.reset() into the episode: same temperatures, rewards and tables as
+    an episode followed by reset_temperatures_philox(episode + 1), over back-to-back episodes
+    (which also exercises the double-buffered pre-pass of the fast path)."""
+    S, N, R, T = 64, 2, 1, 40
+    inp = scenario_batch(S, N, T, seed=13)
+    a, b = _device_for(inp, N, R), _device_for(inp, N, R)
+    for e in range(5):
+        a.run_episode("train", "philox", episode=e, epsilon=0.5, record=("reward",), kernel=kernel, reset_sigma=0.3)
+        b.run_episode("train", "philox", episode=e, epsilon=0.5, record=("reward",), kernel=kernel)
+        b.reset_temperatures_philox(e + 1, 0.3)
+    for x, y in zip(a.get_temperatures(), b.get_temperatures()):
+        assert np.array_equal(x, y)
+    assert np.array_equal(a.get_record("reward"), b.get_record("reward"))
+    assert np.array_equal(a.episode_reward(), b.episode_reward())
+    assert np.array_equal(a.get_q(), b.get_q())
