@@ -240,7 +240,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
-                         "kernel": f"episode_kernel<{N},{'double' if q_bytes == 8 else 'float'}>",
+                         "kernel": eng.last_kernel(),
                          "kernel_ms": kernel_ms,
                          "algorithmic_bytes_per_agent_step": bpa,
                          "algorithmic_bytes_per_launch": bpa * steps_per_episode,

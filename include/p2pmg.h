@@ -154,6 +154,8 @@ int p2pmg_destroy(p2pmg_ctx* ctx);
 const char* p2pmg_last_error(const p2pmg_ctx* ctx);
 int p2pmg_sync(p2pmg_ctx* ctx);
 int p2pmg_device_info(p2pmg_ctx* ctx, char* name, size_t name_len, size_t* total_mem);
+/* which kernel the last episode launch ran, e.g. "episode_fast_kernel<2,f64,R1=2,train>" */
+const char* p2pmg_last_kernel(const p2pmg_ctx* ctx);
 
 /* inputs (host arrays, copied to HBM) */
 int p2pmg_set_env(p2pmg_ctx* ctx, int n_env, const float* time, const float* t_out,

@@ -25,7 +25,7 @@ REC = {"reward": 1, "cost": 2, "grid": 4, "p2p": 8, "t_in": 16, "action": 32, "i
 GREEDY = 255
 
 EXPORTS = [
-    "p2pmg_abi_version", "p2pmg_config_default", "p2pmg_create", "p2pmg_destroy", "p2pmg_last_error",
+    "p2pmg_abi_version", "p2pmg_config_default", "p2pmg_create", "p2pmg_destroy", "p2pmg_last_error", "p2pmg_last_kernel",
     "p2pmg_sync", "p2pmg_device_info", "p2pmg_set_env", "p2pmg_set_profiles", "p2pmg_set_agent_params",
     "p2pmg_set_temperatures", "p2pmg_get_temperatures", "p2pmg_reset_temperatures_philox",
     "p2pmg_set_replay_codes", "p2pmg_zero_q", "p2pmg_set_q", "p2pmg_get_q", "p2pmg_run_episode",
@@ -88,6 +88,7 @@ def _declare(lib):
         "p2pmg_create": ([C.POINTER(Config), i32, C.POINTER(vp)], i32),
         "p2pmg_destroy": ([vp], i32),
         "p2pmg_last_error": ([vp], C.c_char_p),
+        "p2pmg_last_kernel": ([vp], C.c_char_p),
         "p2pmg_sync": ([vp], i32),
         "p2pmg_device_info": ([vp, C.c_char_p, sz, C.POINTER(sz)], i32),
         "p2pmg_set_env": ([vp, i32, fp, fp, fp, fp, fp], i32),

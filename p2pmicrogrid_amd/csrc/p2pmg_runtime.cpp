@@ -95,6 +95,7 @@ struct p2pmg_ctx {
   int64_t d_step = 0;
   int64_t d_added_min = 0;    // every ring holds at least this many transitions
   std::string err;
+  std::string last_kernel;
 };
 
 // ---- RCCL, resolved at run time (torch may already have loaded its own librccl; dlopen by
@@ -695,6 +696,9 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
                      : p2pmg::launch_episode(p, g.q_dtype, c->stream);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));
   c->rec_fast_mask = fast ? (args->record & 127) : 0;
+  c->last_kernel = std::string(fast ? "episode_fast_kernel<" : "episode_kernel<") + std::to_string(c->N) + "," +
+                   (g.q_dtype == 0 ? "f64" : "f32") + ",R1=" + std::to_string(c->R + 1) +
+                   (fast ? (train ? ",train>" : ",greedy>") : (g.shared_q ? ",shared>" : ">"));
   if (!fast) HIP_TRY(c, hipEventRecord(r1, c->stream));
   if (fast) c->pslot ^= 1;
   if (reset && !fast) {  // general kernel: the reset as its own launch
@@ -706,6 +710,8 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   c->n_timed++;
   return P2PMG_OK;
 }
+
+const char* p2pmg_last_kernel(const p2pmg_ctx* c) { return c ? c->last_kernel.c_str() : ""; }
 
 int p2pmg_last_kernel_ms(p2pmg_ctx* c, float* ms) {
   if (!c || !ms) return P2PMG_E_INVALID;

@@ -235,6 +235,10 @@ class DeviceCommunityBatch:
         self._chk(self.L.p2pmg_run_episode(self._ctx, C.byref(args)), "run_episode")
         self._recorded = mask
 
+    def last_kernel(self) -> str:
+        """Name of the kernel the last episode launch ran (fast or general path)."""
+        return (self.L.p2pmg_last_kernel(self._ctx) or b"").decode()
+
     def last_kernel_ms(self) -> float:
         ms = C.c_float(0)
         self._chk(self.L.p2pmg_last_kernel_ms(self._ctx, C.byref(ms)), "last_kernel_ms")
