@@ -64,7 +64,7 @@ def main():
         rows[k] = {"fetch_size_kb_raw": f_kb, "write_size_kb": w_kb,
                    "read_bytes_corrected": 2 * f_kb * 1024, "write_bytes": w_kb * 1024,
                    "hbm_bytes_corrected": (2 * f_kb + w_kb) * 1024}
-    epi = [k for k in rows if "episode_kernel" in k]
+    epi = [k for k in rows if "episode_kernel" in k or "episode_fast_kernel" in k]
     summary = {"round": args.round, "counters": "FETCH_SIZE and WRITE_SIZE in separate rocprofv3 --pmc passes",
                "correction": "reads x2 (gfx950 FETCH_SIZE halving, calibrated on prof_pack_kernel); writes x1",
                "kernels": rows}
