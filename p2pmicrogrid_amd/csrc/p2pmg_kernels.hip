@@ -1271,6 +1271,360 @@ hipError_t launch_fast_q(const EpisodeParams& p, const uint2* pre, void* recs, i
   }
 }
 
+// ----------------------------------------------------------------- the fast shared-table path (N = 16)
+// f64 division with a hoisted reciprocal: hipcc's IEEE f64 sequence (v_div_scale, v_rcp_f64, two
+// Newton steps, q = n * y, r = fma(-d, q, n), v_div_fmas = fma(r, y, q), v_div_fixup) with the
+// scale / fixup steps dropped, which is exact while |n| and |d| lie in [2^-300, 2^300] (the
+// exponent gap stays below the 768 where v_div_scale starts scaling); else the IEEE operator.
+struct Recip64 {
+  double d, y;
+  bool ok;
+};
+__device__ __forceinline__ bool in_div_range64(double x) {
+  const double m = fabs(x);
+  return m >= 0x1p-300 && m <= 0x1p300;
+}
+__device__ __forceinline__ Recip64 recip64(double d) {
+  const double r0 = __builtin_amdgcn_rcp(d);
+  const double r1 = __builtin_fma(r0, __builtin_fma(-d, r0, 1.0), r0);
+  return Recip64{d, __builtin_fma(r1, __builtin_fma(-d, r1, 1.0), r1), in_div_range64(d)};
+}
+__device__ __forceinline__ double fdiv64_ieee(double n, double d) {
+  asm volatile("" : "+v"(n));
+  return n / d;
+}
+__device__ __forceinline__ double fdiv64(double n, const Recip64& r) {
+  const double q = n * r.y;
+  double res = __builtin_fma(__builtin_fma(-r.d, q, n), r.y, q);
+  res = __builtin_copysign(res, q);  // +-0 / d keeps sign(n) * sign(d), as the IEEE quotient
+  if (!(r.ok && (n == 0.0 || in_div_range64(n)))) res = fdiv64_ieee(n, r.d);
+  return res;
+}
+// battery_rule (agent.py:138-153 + storage.py bookkeeping) with the divisions by the agent's
+// capacity, sqrt(efficiency) and 900 s through hoisted reciprocals; same op order, same results
+struct BatK {
+  double smin, smax, se;
+  Recip64 rse, r900;
+};
+__device__ __forceinline__ double battery_rule_r(double balance, double& soc, double cap, const Recip64& rcap,
+                                                 const BatK& b) {
+  const double energy = (balance * 60.0) * 15.0;
+  const double avail_energy = (fmax(0.0, soc - b.smin) * cap) * b.se;
+  const double avail_space = fdiv64(fmax(0.0, b.smax - soc) * cap, b.rse);
+  if (balance > 0.0 && avail_energy > 0.0) {
+    const double x = energy <= avail_energy ? energy : avail_energy;  // min(energy, available_energy)
+    soc = soc - fdiv64(fdiv64(x, rcap), b.rse);
+    balance = balance - fdiv64(x, b.r900);
+  } else if (balance < 0.0 && !(soc >= b.smax)) {
+    const double x = -energy <= avail_space ? -energy : avail_space;
+    soc = soc + b.se * fdiv64(x, rcap);
+    balance = balance + fdiv64(x, b.r900);
+  }
+  return balance;
+}
+
+// episode_sq16_kernel: episode_kernel's shared-table path for 16-agent scenarios (configs[2]),
+// rebuilt for throughput: 1M scenarios keep every SIMD busy, so the cost is instructions per
+// agent-step, not latency.  Same op order and results as episode_kernel (tests compare both).
+//   * round 0 is an even split: round 1's column is the 16 round-0 values of the group, one LDS
+//     write + four 16-B reads instead of a 16 x 16 exchange;
+//   * the divisions of _divide_power share one divisor per round (hoisted reciprocal), the
+//     battery's f64 divisions share the agent's capacity / sqrt(eff) / 900 s reciprocals;
+//   * the final 16 x 16 proposal matrix is transposed through a swizzled LDS tile (4 x 16-B
+//     writes, 16 conflict-free 4-B reads);
+//   * the table is frozen for the episode: TD deltas go to the workgroup's LDS hash as before.
+constexpr int kSq16Waves = 8;                        // waves per workgroup (one hash per 32 scenarios)
+constexpr int kTpStride = 16 * 16 + 16;              // floats per scenario tile (+16: bank offset)
+template <typename QT, int R1, bool TRAIN, bool BAT>
+__global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const EpisodeParams p) {
+  constexpr int N = 16, G = 16, SPW = kWave / G;
+  __shared__ uint32_t hkey[kSqSlots];
+  __shared__ unsigned long long hval[kSqSlots];
+  __shared__ __attribute__((aligned(16))) float tpall[kSq16Waves * SPW * kTpStride];
+  const int wv = (int)(threadIdx.x / kWave);
+  const int lane = (int)(threadIdx.x % kWave);
+  const int sl = lane / G;
+  const int i = lane % G;
+  const int s = (blockIdx.x * kSq16Waves + wv) * SPW + sl;
+  const bool active = s < p.S;
+  const int a = active ? s * N + i : 0;
+  const int s_env = p.n_env == 1 ? 0 : (active ? s : 0);
+  const int T = p.T;
+  const size_t A = (size_t)p.A;
+  const KC k = pin_constants(p);
+  const Dims<true> D{k.nt, k.nT, k.nb, k.np};
+  const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
+  const QT* __restrict__ q = reinterpret_cast<const QT*>(p.q);
+  unsigned long long* const dbase = reinterpret_cast<unsigned long long*>(p.qdelta) +
+                                    (size_t)(blockIdx.x % kDeltaCopies) * n_states * kQPad;
+  for (int k2 = threadIdx.x; k2 < kSqSlots; k2 += kSq16Waves * kWave) {
+    hkey[k2] = kSqEmpty;
+    hval[k2] = 0;
+  }
+  __syncthreads();
+  float* const tp = tpall + (wv * SPW + sl) * kTpStride;  // this scenario's tile
+  // column reads of the transpose: element i of row j sits at j*16 + 4*((i>>2) ^ (j&3)) + (i&3)
+  int cofs[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) cofs[m] = 4 * ((i >> 2) ^ m) + (i & 3);
+
+  const float mi = active ? p.max_in[a] : 1.0f;
+  const Recip rmi = recip(mi), rmph = recip(k.mph), rmargin = recip(k.margin);
+  const float4 lv = p.hp_lv[a];
+  const bool margin_one = p.margin == 1.0f;
+  double bcap = 0.0, soc = 0.0;
+  BatK bk{};
+  Recip64 rcap{};
+  if constexpr (BAT) {
+    bcap = p.bat_cap[a];
+    soc = p.soc[a];
+    bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64(p.bat_sqrt_eff), recip64(900.0)};
+    rcap = recip64(bcap > 0.0 ? bcap : 1.0);
+  }
+  float tin = active ? p.t_in[a] : k.setpoint;
+  float tm = active ? p.t_m[a] : k.setpoint;
+  const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, D.p());
+  const int R1r = p.R + 1, W = (R1r + 3) >> 2;
+
+  const float* envb = p.env + (size_t)s_env * kEnvStride;
+  const size_t env_step = (size_t)p.n_env * kEnvStride;
+  const size_t env_end = env_step * T;
+  const float2* profb = p.prof + a;
+  const size_t prof_end = A * T;
+  const uint32_t* codes_a = p.codes + a;
+  const size_t code_step = (size_t)W * A;
+  auto adv = [](size_t off, size_t step, size_t end) { off += step; return off >= end ? off - end : off; };
+  size_t e1o = adv(0, env_step, env_end), e2o = adv(e1o, env_step, env_end);
+  size_t f1o = adv(0, A, prof_end), f2o = adv(f1o, A, prof_end);
+  size_t c1o = (T > 1) ? code_step : 0;
+  FastRec* const rec_dummy = reinterpret_cast<FastRec*>(p.dummy) + kWave + lane;
+  const bool rec_on = p.record != 0 && active;
+  FastRec* rec_ptr = rec_on ? reinterpret_cast<FastRec*>(p.rec_pack) + a : rec_dummy;
+  const size_t rec_step = rec_on ? A : 0;
+
+  EnvRow e0 = load_env(envb);
+  EnvRow e1 = load_env(envb + e1o);
+  const float2 f0 = profb[0];
+  float2 f1 = profb[f1o];
+  auto step_idx = [&](float time_t, float time_n, float bal, float2 fn, float t_in) {
+    StepIdx st;
+    st.bal = bal;
+    st.baln = fdiv_b(fn.x - fn.y, rmi);
+    const float dt = t_in - k.setpoint;
+    const float tnorm = margin_one ? dt : fdiv_b(dt, rmargin);
+    st.it = idx_time(time_t, D.t());
+    st.iT = idx_temp(tnorm, D.T());
+    st.ib = idx_plain(bal, D.b());
+    st.strip = (uint32_t)(((st.it * D.T() + st.iT) * D.b() + st.ib) * D.p());
+    const int itn = idx_time(time_n, D.t());
+    const int ibn = idx_plain(st.baln, D.b());
+    st.nrow = (uint32_t)(((itn * D.T() + st.iT) * D.b() + ibn) * D.p() + ip_zero);
+    return st;
+  };
+  StepIdx st = step_idx(e0.time, e1.time, fdiv_b(f0.x - f0.y, rmi), f1, tin);
+  uint64_t cw = code_word(p, step_codes(p, codes_a, 0, 0, a, W), active);
+  auto row0_addr = [&](const StepIdx& x, uint64_t c) -> uint32_t {
+    const bool need = ((c & 0xFF) == 255) || (TRAIN && R1 == 1);
+    return need ? x.strip + (uint32_t)ip_zero : x.nrow;
+  };
+  uint32_t a0 = row0_addr(st, cw);
+  Row4<QT> row0 = gather_row(q + a0 * kQPad);
+  Row4<QT> rowN = gather_row(q + (TRAIN ? st.nrow : a0) * kQPad);
+  float ep_sum = 0.0f;
+
+  for (int t = 0; t < T; ++t) {
+    const EnvRow e2 = load_env(envb + e2o);
+    const float2 f2 = profb[f2o];
+    const CodeWords cw1r = step_codes(p, codes_a, c1o, t + 1 == T ? 0 : t + 1, a, W);
+    const float balw = st.bal * mi;
+    float row[N];
+    float col[N];
+
+    // round 0 (P = 0: even split); the battery adjusts the tentative net power
+    int code = (int)(cw & 0xFF);
+    int act = code == 255 ? argmax3(row0) : code;
+    float hp = hp_of(lv, act);
+    int ip = ip_zero;
+    Row4<QT> rowR = row0;
+    uint32_t acts = (uint32_t)act, ips = (uint32_t)ip_zero;
+    double soc_r = soc;
+    float out = balw + hp;
+    if constexpr (BAT) {
+      if (bcap > 0.0) out = (float)battery_rule_r((double)out, soc_r, bcap, rcap, bk);
+    }
+    const float ev0 = div_n<N>(out * 1.0f);
+#pragma unroll
+    for (int j = 0; j < N; ++j) row[j] = ev0;
+    if constexpr (R1 == 2) {
+      // round 1: the column is the group's 16 round-0 values
+      tp[i] = ev0;
+      wave_lds_fence();
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const float4 v = *reinterpret_cast<const float4*>(tp + 4 * m);
+        col[4 * m] = v.x; col[4 * m + 1] = v.y; col[4 * m + 2] = v.z; col[4 * m + 3] = v.w;
+      }
+      wave_lds_fence();
+      float acc = 0.0f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : col[j]));
+      ip = idx_plain(fdiv_b(div_n<N>(acc), rmi), D.p());
+      code = (int)((cw >> 8) & 0xFF);
+      const bool need = code == 255 || TRAIN;
+      rowR = gather_row(q + (need ? st.strip + (uint32_t)ip : a0) * kQPad);
+      act = code == 255 ? argmax3(rowR) : code;
+      acts |= (uint32_t)act << 8;
+      ips |= (uint32_t)ip << 8;
+      hp = hp_of(lv, act);
+      out = balw + hp;
+      soc_r = soc;
+      if constexpr (BAT) {
+        if (bcap > 0.0) out = (float)battery_rule_r((double)out, soc_r, bcap, rcap, bk);
+      }
+      const float flo = out < 0.0f ? 0.0f : -__builtin_inff(), fhi = out > 0.0f ? 0.0f : __builtin_inff();
+      float f[N];
+      float tot = 0.0f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        f[j] = __builtin_amdgcn_fmed3f(-((j == i) ? 0.0f : col[j]), flo, fhi);
+        tot = tot + f[j];
+      }
+      tot = fabsf(tot);
+      const float ev = div_n<N>(out * 1.0f);
+      const Recip rt = recip(tot == 0.0f ? 1.0f : tot);
+      float num[N];
+      bool bad = !rt.ok;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        num[j] = out * fabsf(f[j]);
+        row[j] = fdiv_core(num[j], rt);
+        bad = bad || !fdiv_ok(num[j]);
+      }
+      if (bad) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) row[j] = fdiv_ieee(num[j], rt.b);
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) row[j] = (tot == 0.0f) ? ev : row[j];
+    }
+    soc = soc_r;
+
+    // RC update and the next step's rows
+    float tin1 = tin, tm1 = tm;
+    rc_update(k, e0.t_out, hp, tin1, tm1);
+    const StepIdx st1 = step_idx(e1.time, e2.time, st.baln, f2, tin1);
+    const uint64_t cw1 = code_word(p, cw1r, active);
+    const uint32_t a0n = row0_addr(st1, cw1);
+    const Row4<QT> row0n = gather_row(q + a0n * kQPad);
+    const Row4<QT> rowNn = gather_row(q + (TRAIN ? st1.nrow : a0n) * kQPad);
+
+    // the final P's column through the swizzled tile (community.py:45-54 needs P[j][i])
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      *reinterpret_cast<float4*>(tp + i * 16 + 4 * (m ^ (i & 3))) =
+          make_float4(row[4 * m], row[4 * m + 1], row[4 * m + 2], row[4 * m + 3]);
+    wave_lds_fence();
+#pragma unroll
+    for (int j = 0; j < N; ++j) col[j] = tp[j * 16 + cofs[j & 3]];
+    wave_lds_fence();
+    float g = 0.0f, pp = 0.0f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const float pij = row[j], pji = col[j];
+      const float mn = __builtin_amdgcn_fmed3f(fabsf(pij), fabsf(pji), -__builtin_inff());
+      const bool opp = ((__float_as_uint(pij) ^ __float_as_uint(pji)) >> 31) != 0u;
+      const float ex = opp ? __builtin_copysignf(mn, pij) : 0.0f;
+      g = g + (pij - ex);
+      pp = pp + ex;
+    }
+    float cost = (g >= 0.0f) ? g * e0.buy : g * e0.inj;
+    cost = cost + pp * e0.p2p;
+    cost = fdiv_b(cost * k.slot, rmph);
+    cost = cost * k.kilo;
+    float pen = fmaxf(fmaxf(0.0f, k.lower - tin), fmaxf(0.0f, tin - k.upper));
+    pen = pen > 0.0f ? pen + 1.0f : 0.0f;
+    const float rw = -(cost + k.penw * pen);
+
+    if constexpr (TRAIN) {
+      if (active) {
+        const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
+        const double d = k.alpha * (((double)rw + k.gamma * (double)max3(rowN)) - (double)qsa);
+        lds_add_by_key(hkey, hval, (st.strip + (uint32_t)ip) * kQPad + (uint32_t)act, __double2ll_rn(d * kDeltaScale),
+                       dbase);
+      }
+    }
+    {
+      const uint32_t bins = (uint32_t)(st.it * D.T() * D.b() + st.ib) | ((uint32_t)st.iT << 16);
+      float4* rp = reinterpret_cast<float4*>(rec_ptr);
+      rp[0] = make_float4(rw, cost, g, pp);
+      rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
+      rec_ptr += rec_step;
+    }
+    // avg_reward = sum_t mean_i r (community.py:179): the group's rewards in agent order
+    tp[i] = rw;
+    wave_lds_fence();
+    float msum = 0.0f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float4 v = *reinterpret_cast<const float4*>(tp + 4 * m);
+      msum = msum + v.x; msum = msum + v.y; msum = msum + v.z; msum = msum + v.w;
+    }
+    wave_lds_fence();
+    ep_sum = ep_sum + div_n<N>(msum);
+
+    tin = tin1;
+    tm = tm1;
+    e0 = e1;
+    e1 = e2;
+    f1 = f2;
+    e2o = adv(e2o, env_step, env_end);
+    f2o = adv(f2o, A, prof_end);
+    c1o = (t + 2 >= T) ? (size_t)0 : c1o + code_step;
+    st = st1;
+    cw = cw1;
+    a0 = a0n;
+    row0 = row0n;
+    rowN = rowNn;
+  }
+  if (active) {
+    if (p.reset_t0)
+      t0_draw(p.seed_lo, p.seed_hi, p.episode + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, tin, tm);
+    p.t_in[a] = tin;
+    p.t_m[a] = tm;
+    if constexpr (BAT) p.soc[a] = soc;
+    if (i == 0) p.ep_reward[s] = ep_sum;
+  }
+  if constexpr (TRAIN) {  // flush the episode's sums into this XCD's replica
+    __syncthreads();
+    for (int k2 = threadIdx.x; k2 < kSqSlots; k2 += kSq16Waves * kWave) {
+      const uint32_t key = hkey[k2];
+      const long long x = (long long)hval[k2];
+      if (key != kSqEmpty && x != 0) atomicAdd(dbase + key, (unsigned long long)x);
+    }
+  }
+}
+
+template <typename QT, int R1>
+void launch_sq16_r(const EpisodeParams& p, int blocks, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  const dim3 g(blocks), b(kWave * kSq16Waves);
+  if (p.mode == 0) {
+    if (p.battery) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, true>), g, b, 0, st, ev0, ev1, 0, p);
+    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, false>), g, b, 0, st, ev0, ev1, 0, p);
+  } else {
+    if (p.battery) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, true>), g, b, 0, st, ev0, ev1, 0, p);
+    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, false>), g, b, 0, st, ev0, ev1, 0, p);
+  }
+}
+template <typename QT>
+hipError_t launch_sq16_q(const EpisodeParams& p, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  const int waves = (p.S + kWave / 16 - 1) / (kWave / 16);
+  const int blocks = (waves + kSq16Waves - 1) / kSq16Waves;
+  if (p.R == 0) launch_sq16_r<QT, 1>(p, blocks, ev0, ev1, st);
+  else if (p.R == 1) launch_sq16_r<QT, 2>(p, blocks, ev0, ev1, st);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 template <int N, typename QT, bool SQ>
 void launch_nq(const EpisodeParams& p, hipStream_t st) {
   constexpr int SPW = kWave / pow2ceil(N);
@@ -1442,6 +1796,10 @@ hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void*
   hipLaunchKernelGGL(fast_rec_unpack_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, T, R1, A, tb,
                      reinterpret_cast<const FastRec*>(recs), which, out);
   return hipGetLastError();
+}
+
+hipError_t launch_episode_sq16(const EpisodeParams& p, int q_dtype, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream) {
+  return q_dtype == 0 ? launch_sq16_q<double>(p, ev0, ev1, stream) : launch_sq16_q<float>(p, ev0, ev1, stream);
 }
 
 hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream) {

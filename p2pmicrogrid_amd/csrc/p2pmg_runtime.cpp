@@ -628,6 +628,11 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
                     (long long)c->T * c->A < (1LL << 32) && host_div_range(g.minutes_per_hour) &&
                     host_div_range(g.temp_margin) &&
                     !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_PHILOX_INKERNEL)) && !env_general;
+  // shared table, 16-agent scenarios (configs[2]): episode_sq16_kernel
+  const bool sq16 = g.shared_q && c->N == 16 && c->R <= 1 && c->mi_ok && host_div_range(g.minutes_per_hour) &&
+                    host_div_range(g.temp_margin) && g.n_time_states == 20 && g.n_temp_states == 20 &&
+                    g.n_balance_states == 20 && g.n_p2p_states == 20 &&
+                    !(args->flags & P2PMG_FLAG_GENERAL_KERNEL) && !env_general;
   const int ps = c->pslot;
   p2pmg::PrepOut next{};
   bool produce = false;
@@ -661,7 +666,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     c->spec_episode[ns] = philox ? args->episode + 1 : -1;
     c->spec_eps[ns] = args->epsilon;
   } else if (train && args->rng == P2PMG_RNG_PHILOX) {
-    bool prepass = c->A < (1 << 18);
+    bool prepass = c->A < (1 << 18) && !sq16;  // sq16: throughput-bound, draws in the kernel
     if (args->flags & P2PMG_FLAG_PHILOX_PREPASS) prepass = true;
     if (args->flags & P2PMG_FLAG_PHILOX_INKERNEL) prepass = false;
     if (prepass) {
@@ -680,7 +685,13 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   }
   const int slot = (int)(c->n_timed % p2pmg_ctx::kRing);
   hipEvent_t r0 = c->ring[2 * slot], r1 = c->ring[2 * slot + 1];
-  if (!fast) HIP_TRY(c, hipEventRecord(r0, c->stream));
+  if (sq16) {
+    if (args->record && !c->rec_pack)
+      HIP_TRY(c, hipMalloc(&c->rec_pack, (size_t)c->T * c->A * p2pmg::kFastRecBytes));
+    p.rec_pack = c->rec_pack;
+  }
+  const bool ext = fast || sq16;  // launches that stamp their own timing events
+  if (!ext) HIP_TRY(c, hipEventRecord(r0, c->stream));
   int spw = args->scen_per_wave > 0 ? args->scen_per_wave : env_spw;
   if (spw <= 0) {  // automatic: full waves, or spread a small batch over all CUs (one wave per CU)
     const int full = 64 / (c->N <= 1 ? 1 : c->N <= 2 ? 2 : c->N <= 4 ? 4 : 8);
@@ -689,19 +700,21 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     spw = std::min(spw, full);
   }
   const bool reset = (args->flags & P2PMG_FLAG_RESET_T0) != 0;
-  p.reset_t0 = (fast && reset) ? 1 : 0;
+  p.reset_t0 = (ext && reset) ? 1 : 0;
   p.reset_sigma = args->reset_sigma;
-  hipError_t e = fast ? p2pmg::launch_episode_fast(p, c->pre[ps], c->rec_pack, g.q_dtype, spw,
-                                                  produce ? &next : nullptr, r0, r1, c->stream)
-                     : p2pmg::launch_episode(p, g.q_dtype, c->stream);
+  hipError_t e = fast   ? p2pmg::launch_episode_fast(p, c->pre[ps], c->rec_pack, g.q_dtype, spw,
+                                                    produce ? &next : nullptr, r0, r1, c->stream)
+                 : sq16 ? p2pmg::launch_episode_sq16(p, g.q_dtype, r0, r1, c->stream)
+                        : p2pmg::launch_episode(p, g.q_dtype, c->stream);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));
-  c->rec_fast_mask = fast ? (args->record & 127) : 0;
-  c->last_kernel = std::string(fast ? "episode_fast_kernel<" : "episode_kernel<") + std::to_string(c->N) + "," +
-                   (g.q_dtype == 0 ? "f64" : "f32") + ",R1=" + std::to_string(c->R + 1) +
-                   (fast ? (train ? ",train>" : ",greedy>") : (g.shared_q ? ",shared>" : ">"));
-  if (!fast) HIP_TRY(c, hipEventRecord(r1, c->stream));
+  c->rec_fast_mask = ext ? (args->record & 127) : 0;
+  c->last_kernel = std::string(fast ? "episode_fast_kernel<" : sq16 ? "episode_sq16_kernel<" : "episode_kernel<") +
+                   std::to_string(c->N) + "," + (g.q_dtype == 0 ? "f64" : "f32") + ",R1=" + std::to_string(c->R + 1) +
+                   (ext ? (train ? ",train" : ",greedy") : "") + (g.shared_q ? ",shared" : "") +
+                   (c->battery ? ",battery>" : ">");
+  if (!ext) HIP_TRY(c, hipEventRecord(r1, c->stream));
   if (fast) c->pslot ^= 1;
-  if (reset && !fast) {  // general kernel: the reset as its own launch
+  if (reset && !ext) {  // general kernel: the reset as its own launch
     const uint32_t off = (uint32_t)(g.scenario_offset * c->N);
     HIP_TRY(c, p2pmg::launch_t0_philox(c->A, c->t_in, c->t_m, p.seed_lo, p.seed_hi, args->episode + 1, off,
                                        g.setpoint, args->reset_sigma, c->stream));

@@ -96,3 +96,36 @@ def test_rccl_allreduce_world1_is_identity():
     eng.apply_q_delta()
     ob.apply_q_delta()
     assert np.array_equal(eng.get_q(dtype=np.float32).reshape(ob.q.shape), ob.q)
+
+
+@pytest.mark.parametrize("q_dtype,battery,R", [("f32", True, 1), ("f64", False, 1), ("f32", True, 0)])
+def test_sq16_kernel_matches_general_kernel(q_dtype, battery, R):
+    """configs[2] runs on episode_sq16_kernel; the general episode_kernel (checked against the
+    oracle above) must give the same records, deltas, SoC and temperatures on a ragged batch."""
+    S, T = 701, 40  # 701: a partial last wave and a partial last workgroup
+    a, _ = _setup(S, 16, R, T, q_dtype, True, battery, False, seed=3)
+    b, _ = _setup(S, 16, R, T, q_dtype, True, battery, False, seed=3)
+    dt = np.float64 if q_dtype == "f64" else np.float32
+    for e in range(3):
+        philox = "prepass" if e == 1 else "auto"
+        a.run_episode("train", "philox", episode=e, epsilon=0.5, record=REC, philox=philox, reset_sigma=0.3)
+        b.run_episode("train", "philox", episode=e, epsilon=0.5, record=REC, philox=philox, reset_sigma=0.3,
+                      kernel="general")
+        assert "sq16" in a.last_kernel() and "sq16" not in b.last_kernel()
+        ra, rb = a.get_records(REC), b.get_records(REC)
+        for k in REC:
+            assert np.array_equal(ra[k], rb[k]), (e, k)
+        assert np.array_equal(a.get_q_delta(), b.get_q_delta()), e
+        assert np.array_equal(a.episode_reward(), b.episode_reward()), e
+        if battery:
+            assert np.array_equal(a.get_soc(), b.get_soc()), e
+        for x, y in zip(a.get_temperatures(), b.get_temperatures()):
+            assert np.array_equal(x, y), e
+        a.apply_q_delta()
+        b.apply_q_delta()
+        assert np.array_equal(a.get_q(dtype=dt), b.get_q(dtype=dt))
+    a.run_episode("greedy", record=REC)
+    b.run_episode("greedy", record=REC, kernel="general")
+    ra, rb = a.get_records(REC), b.get_records(REC)
+    for k in REC:
+        assert np.array_equal(ra[k], rb[k]), ("greedy", k)
