@@ -358,12 +358,15 @@ constexpr int kSqWaves = 4;          // waves per workgroup
 constexpr int kSqSlotBits = 11;      // 2048 slots: 8 KB keys + 16 KB sums
 constexpr int kSqSlots = 1 << kSqSlotBits;
 constexpr uint32_t kSqEmpty = 0xFFFFFFFFu;
+constexpr int kSqProbes = 16;      // linear-probe limit before the global fallback
+constexpr int kSqFlushSteps = 8;    // steps between flushes of the LDS table
 
 __device__ __forceinline__ void lds_add_by_key(uint32_t* hk, unsigned long long* hv, uint32_t key, long long v,
                                                unsigned long long* gbase) {
   if (v == 0) return;
   uint32_t h = (key * 2654435761u) >> (32 - kSqSlotBits);
-  for (int probe = 0; probe < 32; ++probe) {
+#pragma nounroll
+  for (int probe = 0; probe < kSqProbes; ++probe) {
     const uint32_t prev = atomicCAS(hk + h, kSqEmpty, key);
     if (prev == kSqEmpty || prev == key) {
       atomicAdd(hv + h, (unsigned long long)v);
@@ -371,7 +374,26 @@ __device__ __forceinline__ void lds_add_by_key(uint32_t* hk, unsigned long long*
     }
     h = (h + 1) & (kSqSlots - 1);
   }
-  atomicAdd(gbase + key, (unsigned long long)v);  // crowded table: straight to the global replica
+  atomicAdd(gbase + key, (unsigned long long)v);  // crowded run of slots: straight to the global replica
+}
+// Block-uniform: move the table's sums into the XCD's replica and empty it.  Called every
+// kSqFlushSteps steps, not once per episode: a 32-scenario workgroup touches ~3.2k distinct
+// (state, action) keys per 96-step episode (more than the 2048 slots) but only ~600 in any
+// 8-step window, because the time bin moves on; the total number of global atomics grows by
+// ~15 % while the table stays below a third full, so a probe run is ~1 slot long.
+__device__ __forceinline__ void lds_hash_flush(uint32_t* hk, unsigned long long* hv, unsigned long long* gbase,
+                                               int nthreads) {
+  __syncthreads();
+  for (int k2 = threadIdx.x; k2 < kSqSlots; k2 += nthreads) {
+    const uint32_t key = hk[k2];
+    if (key != kSqEmpty) {
+      const long long x = (long long)hv[k2];
+      if (x != 0) atomicAdd(gbase + key, (unsigned long long)x);
+      hk[k2] = kSqEmpty;
+      hv[k2] = 0;
+    }
+  }
+  __syncthreads();
 }
 
 // timing-only ablations of the fast kernel's gathers: 7 = round-R gather fake, 8 = prefetched rows fake
@@ -621,6 +643,9 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
     // avg_reward = sum_t mean_i r (community.py:179), canonical sequential order
     const float m = group_sum<N>(rw, lane, i, sl, shR);
     ep_sum = ep_sum + div_n<N>(m);
+    if constexpr (SQ) {
+      if (train && (t % kSqFlushSteps == kSqFlushSteps - 1 || t + 1 == T)) lds_hash_flush(hkey, hval, dbase, WPB * kWave);
+    }
 
     tin = tin1;
     tm = tm1;
@@ -642,16 +667,6 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
     p.t_m[a] = tm;
     if (bat) p.soc[a] = soc;
     if (i == 0) p.ep_reward[s] = ep_sum;
-  }
-  if constexpr (SQ) {
-    if (train) {  // block-uniform: flush the episode's sums into this XCD's replica
-      __syncthreads();
-      for (int k2 = threadIdx.x; k2 < kSqSlots; k2 += WPB * kWave) {
-        const uint32_t key = hkey[k2];
-        const long long x = (long long)hval[k2];
-        if (key != kSqEmpty && x != 0) atomicAdd(dbase + key, (unsigned long long)x);
-      }
-    }
   }
 }
 
@@ -1571,6 +1586,9 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
     }
     wave_lds_fence();
     ep_sum = ep_sum + div_n<N>(msum);
+    if constexpr (TRAIN) {
+      if (t % kSqFlushSteps == kSqFlushSteps - 1 || t + 1 == T) lds_hash_flush(hkey, hval, dbase, kSq16Waves * kWave);
+    }
 
     tin = tin1;
     tm = tm1;
@@ -1593,14 +1611,6 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
     p.t_m[a] = tm;
     if constexpr (BAT) p.soc[a] = soc;
     if (i == 0) p.ep_reward[s] = ep_sum;
-  }
-  if constexpr (TRAIN) {  // flush the episode's sums into this XCD's replica
-    __syncthreads();
-    for (int k2 = threadIdx.x; k2 < kSqSlots; k2 += kSq16Waves * kWave) {
-      const uint32_t key = hkey[k2];
-      const long long x = (long long)hval[k2];
-      if (key != kSqEmpty && x != 0) atomicAdd(dbase + key, (unsigned long long)x);
-    }
   }
 }
 
