@@ -92,7 +92,113 @@ WORKLOADS = {
     # name: (scenarios per GPU, agents, rounds R, horizon, q dtype, shared table, battery)
     "config2": (4096, 2, 1, 96, "f64", False, False),
     "config3": (125000, 16, 1, 96, "f32", True, True),
+    "config5": (4096, 2, 1, 96, "f32", True, False),  # DQN, one shared network (data-parallel)
 }
+
+MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_16x16x4_f32) = f32 vector rate
+DQN_FWD_FLOP = 2 * (5 * 64 + 64 * 64 + 64 * 1)  # QNetwork (rl.py:135-148): 8,960 FLOP per row
+
+
+def dqn_flop_per_agent_step(R: int) -> int:
+    """Trainer._train (rl.py:307-333) = 3 target forwards x 32 samples +
+    1 online forward + backward (2x forward) x 32 = 32 * 6 * 8,960; the greedy action choice
+    adds 3 forwards per negotiation round (ActorModel rl.py:186-194)."""
+    return 32 * 6 * DQN_FWD_FLOP + 3 * (R + 1) * DQN_FWD_FLOP
+
+
+def cpu_baseline_dqn(seconds: float, S: int = 2, N: int = 2, R: int = 1, T: int = 96):
+    """oracle/dqn.py (NumPy, one thread) on a bounded sample: one fill episode, then train episodes."""
+    from oracle import dqn as odqn
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    inp = scenario_batch(S, N, T)
+    th0 = odqn.glorot_init(1, 0)
+    ob = odqn.OracleDQNBatch(S=S, N=N, R=R, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in,
+                             env_time=inp.time[None], env_tout=inp.t_out, theta0=th0, shared=True)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    ob.run_episode("fill", rng="philox", episode=0, eps=1.0)
+    t0 = time.perf_counter()
+    done = 0
+    while True:
+        ob.run_episode("train", rng="philox", episode=1 + done, eps=0.9 ** (1 + done))
+        done += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": S * N * T * done / dt, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{S} scenarios x N={N} DQN agents (R={R}, T={T}, shared network), {done} training "
+                      f"episodes after one fill episode, oracle/dqn.py NumPy, {dt:.1f} s"}
+
+
+def main_dqn(args, rank, world, local, S, N, R, T):
+    """configs[4]: DQN agents with ONE shared Q-network (data-parallel): every env step runs the
+    act launch (greedy forwards on the Q-MLP, market, reward, replay append, RC update) and the
+    train launch (32-sample batches on f32 MFMA) + gradient reduce (+ RCCL all-reduce over ranks)
+    + Adam/soft update.  One bench step = one training episode (T env steps) of every scenario."""
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    from p2pmicrogrid_amd.dqn import DeviceDQNBatch
+    first = rank * S
+    inp = scenario_batch(S, N, T, first_scenario=first)
+    eng = DeviceDQNBatch(S, N, R, T, shared=True, device=local, scenario_offset=first, init_seed=0)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    del inp
+    if world > 1:
+        from p2pmicrogrid_amd.distributed import broadcast_bytes
+        from p2pmicrogrid_amd.engine import comm_unique_id
+        eng.comm_init(broadcast_bytes(comm_unique_id() if rank == 0 else None, world), rank, world)
+    record = ("reward", "cost")
+    eng.run_episode("fill", "philox", episode=0, epsilon=1.0, record=record)  # community.init_buffers
+    eng.reset_temperatures_philox(1, 0.3)
+
+    def episode(e):  # rl.py:196-197: epsilon 1 x 0.9 per episode, no floor
+        eng.run_episode("train", "philox", episode=e, epsilon=0.9 ** e, record=record)
+        eng.reset_temperatures_philox(e + 1, 0.3)
+
+    for e in range(1, 1 + args.warmup):
+        episode(e)
+    eng.sync()
+    eng.reset_kernel_times()
+    barrier(world)
+    eng.sync()
+    t0 = time.perf_counter()
+    for e in range(1 + args.warmup, 1 + args.warmup + args.steps):
+        episode(e)
+    eng.sync()
+    barrier(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    kms = eng.kernel_times()
+    steps_per_episode = S * N * T
+    flop = dqn_flop_per_agent_step(R)
+    episode_ms = float(np.mean(kms)) if len(kms) else float("nan")
+    achieved = flop * steps_per_episode / (episode_ms * 1e-3) / 1e12
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": world * steps_per_episode * args.steps / dt, "unit": "agent-steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic profiles with the reference dataset schema (seed 42), Glorot-uniform init",
+            "config": {"workload": f"configs[4]: {S} scenarios/GPU x {N} DQN agents (R={R}, T={T}), one shared "
+                                   f"5-64-64-1 Q-network, 32-sample batches per agent-step, Adam + soft update "
+                                   f"per step, gradient all-reduce over ranks (RCCL)",
+                       "scenarios_per_gpu": S, "agents_per_scenario": N, "rounds": R + 1, "horizon": T,
+                       "agent_steps_per_step": world * steps_per_episode,
+                       "parallelism": f"scenario-sharded x{world}, data-parallel shared network"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": achieved / MFMA_F32_PEAK_TFS, "traffic": None,
+                         "kernel": "DQN episode: T x (dqn_act_kernel + dqn_train_kernel + reduce + adam)",
+                         "kernel_ms": episode_ms, "flop_per_agent_step": flop,
+                         "flop_per_episode": flop * steps_per_episode, "timed_launches": int(len(kms))},
+            "mean_episode_reward": float(np.mean(eng.episode_reward())),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_dqn(args.cpu_seconds, R=R, T=T)
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 96, q_dtype: str = "f64",
@@ -149,7 +255,8 @@ def main():
     ap.add_argument("--q-dtype", default=None, choices=["f64", "f32"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary for roofline.traffic (default profiles/pmc_traffic[_<workload>].json)")
     args = ap.parse_args()
 
     rank, world, local = dist_setup()
@@ -162,6 +269,8 @@ def main():
     R = R if args.rounds is None else args.rounds
     T = args.horizon or T
     q_dtype = args.q_dtype or q_dtype
+    if args.workload == "config5":
+        return main_dqn(args, rank, world, local, S, N, R, T)
     first = rank * S
     inp = scenario_batch(S, N, T, first_scenario=first)
     eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=local, scenario_offset=first, shared_q=shared)
@@ -217,7 +326,9 @@ def main():
                     f"{q_dtype} Q-tables, Philox exploration, train episodes")
     kernel_ms = float(np.mean(kms)) if len(kms) else float("nan")
     achieved = bpa * steps_per_episode / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.traffic_json, workload)
+    tj = args.traffic_json or os.path.join(
+        ROOT, "profiles", "pmc_traffic.json" if args.workload == "config2" else f"pmc_traffic_{args.workload}.json")
+    traffic = load_traffic(tj, workload)
     if rank == 0:
         out = {
             "metric": METRIC,

@@ -491,12 +491,26 @@ __global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
   }
 }
 
-// shared network: sum the workgroup partials in a fixed order
-__global__ void dqn_reduce_kernel(const DqnParams d, int n_partials) {
+// shared network: sum the workgroup partials in a fixed order, in two levels so the sum is
+// parallel over both the 4609 parameters and the partials: level 1 (grid.y = kRedChunks) folds
+// each run of `per` consecutive partials sequentially into the run's first row, in place (one
+// thread owns one (run, parameter) cell); level 2 adds the runs' results in run order.
+constexpr int kRedChunks = 64;
+__global__ void dqn_reduce_chunks_kernel(const DqnParams d, int n_partials, int per) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b0 = blockIdx.y * per;
+  if (k >= kDqnParams || b0 >= n_partials) return;
+  const int b1 = min(n_partials, b0 + per);
+  float* g = d.grad + k;
+  float s = 0.0f;
+  for (int b = b0; b < b1; ++b) s += g[(size_t)b * kNetStride];
+  g[(size_t)b0 * kNetStride] = s;
+}
+__global__ void dqn_reduce_kernel(const DqnParams d, int n_partials, int per) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= kDqnParams) return;
   float s = 0.0f;
-  for (int b = 0; b < n_partials; ++b) s += d.grad[(size_t)b * kNetStride + k];
+  for (int b = 0; b < n_partials; b += per) s += d.grad[(size_t)b * kNetStride + k];
   d.gsum[k] = s;
 }
 
@@ -559,7 +573,12 @@ hipError_t launch_dqn_train(const DqnParams& d, int blocks, bool shared_partials
 }
 
 hipError_t launch_dqn_reduce(const DqnParams& d, int n_partials, hipStream_t st) {
-  hipLaunchKernelGGL(dqn_reduce_kernel, dim3((kDqnParams + 255) / 256), dim3(256), 0, st, d, n_partials);
+  const int per = (n_partials + kRedChunks - 1) / kRedChunks;
+  if (per > 1) {
+    hipLaunchKernelGGL(dqn_reduce_chunks_kernel, dim3((kDqnParams + 255) / 256, kRedChunks), dim3(256), 0, st, d,
+                       n_partials, per);
+  }
+  hipLaunchKernelGGL(dqn_reduce_kernel, dim3((kDqnParams + 255) / 256), dim3(256), 0, st, d, n_partials, per);
   return hipGetLastError();
 }
 
