@@ -52,6 +52,7 @@ struct EpisodeParams {
   void* dummy;               // >= 2 * kWave * 32 B scratch: target of the fast kernel's masked-off stores
   uint32_t* pre_ipc;         // fast path, N = 2: [T][A] round-1 p2p bins for the partner's 3 round-0 actions
   void* rec_pack;            // fast paths: packed records [T][A] x 32 B
+  int rec_narrow;            // sq16: only reward + cost requested -> rec_pack is [T][A] float2
   int reset_t0;              // fast path: draw T0 for episode + 1 at the end (P2PMG_FLAG_RESET_T0)
   double reset_sigma;
   int nt, nT, nb, np;
@@ -123,7 +124,7 @@ hipError_t launch_episode_fast(const EpisodeParams& p, const uint2* pre, void* r
 hipError_t launch_episode_sq16(const EpisodeParams& p, int q_dtype, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
 constexpr size_t kFastRecBytes = 32;  // one packed record row per agent-step (FastRec)
 // which: 0..4 reward, cost, grid, p2p, tin ([T][A] f32); 5 action (u8), 6 index (i32) [T][R+1][A]
-hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void* recs, int which, void* out,
+hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void* recs, int narrow, int which, void* out,
                                   hipStream_t stream);
 hipError_t launch_apply_delta(void* q, long long* qdelta, size_t n, int q_dtype, hipStream_t stream);
 hipError_t launch_fold_delta(long long* qdelta, size_t n, hipStream_t stream);

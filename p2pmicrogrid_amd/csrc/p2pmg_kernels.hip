@@ -1216,10 +1216,15 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
 
 // FastRec rows -> the general record buffers (reward, cost, grid, p2p, tin [T][A]; action u8 and
 // packed index i32 [T][R+1][A]), for the records the caller asks for
-__global__ void fast_rec_unpack_kernel(int T, int R1, int A, uint32_t tb, const FastRec* __restrict__ recs, int which,
-                                       void* __restrict__ out) {
+__global__ void fast_rec_unpack_kernel(int T, int R1, int A, uint32_t tb, const FastRec* __restrict__ recs, int narrow,
+                                       int which, void* __restrict__ out) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
   if (k >= (size_t)T * A) return;
+  if (narrow) {  // [T][A] float2 {reward, cost}
+    const float2 v = reinterpret_cast<const float2*>(recs)[k];
+    reinterpret_cast<float*>(out)[k] = which == 0 ? v.x : v.y;
+    return;
+  }
   const FastRec r = recs[k];
   if (which < 5) {
     const float v[5] = {r.reward, r.cost, r.grid, r.p2p, r.tin};
@@ -1412,10 +1417,14 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
   size_t e1o = adv(0, env_step, env_end), e2o = adv(e1o, env_step, env_end);
   size_t f1o = adv(0, A, prof_end), f2o = adv(f1o, A, prof_end);
   size_t c1o = (T > 1) ? code_step : 0;
-  FastRec* const rec_dummy = reinterpret_cast<FastRec*>(p.dummy) + kWave + lane;
+  // records: FastRec rows, or only {reward, cost} as float2 when nothing else was requested
+  // (8 B instead of 32 B of writes per agent-step); masked-off lanes write a dummy row
+  const bool narrow = p.rec_narrow != 0;
+  const size_t rec_bytes = narrow ? sizeof(float2) : sizeof(FastRec);
+  char* const rec_dummy = reinterpret_cast<char*>(reinterpret_cast<FastRec*>(p.dummy) + kWave + lane);
   const bool rec_on = p.record != 0 && active;
-  FastRec* rec_ptr = rec_on ? reinterpret_cast<FastRec*>(p.rec_pack) + a : rec_dummy;
-  const size_t rec_step = rec_on ? A : 0;
+  char* rec_ptr = rec_on ? reinterpret_cast<char*>(p.rec_pack) + (size_t)a * rec_bytes : rec_dummy;
+  const size_t rec_step = rec_on ? A * rec_bytes : 0;
 
   EnvRow e0 = load_env(envb);
   EnvRow e1 = load_env(envb + e1o);
@@ -1568,13 +1577,15 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
                        dbase);
       }
     }
-    {
+    if (narrow) {
+      *reinterpret_cast<float2*>(rec_ptr) = make_float2(rw, cost);
+    } else {
       const uint32_t bins = (uint32_t)(st.it * D.T() * D.b() + st.ib) | ((uint32_t)st.iT << 16);
       float4* rp = reinterpret_cast<float4*>(rec_ptr);
       rp[0] = make_float4(rw, cost, g, pp);
       rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
-      rec_ptr += rec_step;
     }
+    rec_ptr += rec_step;
     // avg_reward = sum_t mean_i r (community.py:179): the group's rewards in agent order
     tp[i] = rw;
     wave_lds_fence();
@@ -1799,12 +1810,12 @@ hipError_t launch_episode_fast(const EpisodeParams& p, const uint2* pre, void* r
                       : launch_fast_q<float>(p, pre, recs, spw, next, ev0, ev1, stream);
 }
 
-hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void* recs, int which, void* out,
+hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void* recs, int narrow, int which, void* out,
                                   hipStream_t stream) {
   const size_t n = (size_t)T * A;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(fast_rec_unpack_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, T, R1, A, tb,
-                     reinterpret_cast<const FastRec*>(recs), which, out);
+                     reinterpret_cast<const FastRec*>(recs), narrow, which, out);
   return hipGetLastError();
 }
 

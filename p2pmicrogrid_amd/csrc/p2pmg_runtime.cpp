@@ -61,6 +61,7 @@ struct p2pmg_ctx {
   void* dummy = nullptr;      // fast path: target of masked-off stores (2 * 64 * 32 B)
   void* rec_pack = nullptr;   // fast path: packed records [T][A] x 32 B
   int rec_fast_mask = 0;      // records of the last episode that live (packed) in rec_pack
+  int rec_narrow = 0;         // ... as [T][A] float2 {reward, cost} (sq16 with only those two requested)
   int code_src = 0;          // what the code buffer holds: 0 none, 1 replay upload, 2 Philox pre-pass
   float* ep_reward = nullptr;
   float* rec_f32[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // reward, cost, grid, p2p, tin
@@ -689,6 +690,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     if (args->record && !c->rec_pack)
       HIP_TRY(c, hipMalloc(&c->rec_pack, (size_t)c->T * c->A * p2pmg::kFastRecBytes));
     p.rec_pack = c->rec_pack;
+    p.rec_narrow = (args->record & ~(P2PMG_REC_REWARD | P2PMG_REC_COST)) == 0 ? 1 : 0;
   }
   const bool ext = fast || sq16;  // launches that stamp their own timing events
   if (!ext) HIP_TRY(c, hipEventRecord(r0, c->stream));
@@ -708,6 +710,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
                         : p2pmg::launch_episode(p, g.q_dtype, c->stream);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));
   c->rec_fast_mask = ext ? (args->record & 127) : 0;
+  c->rec_narrow = sq16 ? p.rec_narrow : 0;
   c->last_kernel = std::string(fast ? "episode_fast_kernel<" : sq16 ? "episode_sq16_kernel<" : "episode_kernel<") +
                    std::to_string(c->N) + "," + (g.q_dtype == 0 ? "f64" : "f32") + ",R1=" + std::to_string(c->R + 1) +
                    (ext ? (train ? ",train" : ",greedy") : "") + (g.shared_q ? ",shared" : "") +
@@ -782,7 +785,7 @@ int p2pmg_get_record(p2pmg_ctx* c, int which, void* host) {
   if (c->rec_fast_mask & which) {  // the last episode ran the fast kernel: unpack its rows
     const int w = slot >= 0 ? slot : (which == P2PMG_REC_ACTION ? 5 : 6);
     const uint32_t tb = (uint32_t)(c->cfg.n_temp_states * c->cfg.n_balance_states);
-    HIP_TRY(c, p2pmg::launch_fast_rec_unpack(c->T, c->R + 1, c->A, tb, c->rec_pack, w, const_cast<void*>(src), c->stream));
+    HIP_TRY(c, p2pmg::launch_fast_rec_unpack(c->T, c->R + 1, c->A, tb, c->rec_pack, c->rec_narrow, w, const_cast<void*>(src), c->stream));
   }
   HIP_TRY(c, hipMemcpyAsync(host, src, bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -129,3 +129,9 @@ def test_sq16_kernel_matches_general_kernel(q_dtype, battery, R):
     ra, rb = a.get_records(REC), b.get_records(REC)
     for k in REC:
         assert np.array_equal(ra[k], rb[k]), ("greedy", k)
+    # only reward + cost requested: sq16 writes the narrow float2 record rows
+    a.run_episode("train", "philox", episode=5, epsilon=0.5, record=("reward", "cost"))
+    b.run_episode("train", "philox", episode=5, epsilon=0.5, record=("reward", "cost"), kernel="general")
+    for k in ("reward", "cost"):
+        assert np.array_equal(a.get_record(k), b.get_record(k)), ("narrow", k)
+    assert np.array_equal(a.get_q_delta(), b.get_q_delta())
