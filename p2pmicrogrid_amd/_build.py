@@ -42,7 +42,7 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=())
     if out == LIB and not defines and not force and not needs_build():
         return LIB
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
+           "-Wall", "-Wno-unused-function", "-Wno-pass-failed", f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
            *[f"-D{d}" for d in defines], *[os.path.join(CSRC, s) for s in SOURCES], "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)

@@ -236,6 +236,14 @@ __device__ __forceinline__ KC pin_constants(const EpisodeParams& p) {
   return k;
 }
 
+// The same constants left to the compiler (kernel arguments stay in SGPRs): the throughput-bound
+// sq16 kernel runs several waves per SIMD, where VGPRs, not the scalar-operand latency, set the pace.
+__device__ __forceinline__ KC scalar_constants(const EpisodeParams& p) {
+  return KC{p.setpoint, p.margin, p.lower, p.upper, p.inv_ci, p.inv_cm, p.inv_ri, p.inv_re, p.inv_rvent,
+            p.c_in,     p.c_m,    p.solar, p.cop,   p.spm,    p.slot,   p.mph,    p.kilo,   p.penw,
+            p.alpha,    p.gamma,  p.nt,    p.nT,    p.nb,     p.np};
+}
+
 // Everything about step t that is known before its negotiation starts.
 struct StepIdx {
   float bal;        // (load - pv) / max_in of this step    agent.py:172-176
@@ -1292,6 +1300,23 @@ hipError_t launch_fast_q(const EpisodeParams& p, const uint2* pre, void* recs, i
 }
 
 // ----------------------------------------------------------------- the fast shared-table path (N = 16)
+typedef float pkf2 __attribute__((ext_vector_type(2)));
+// 0 or |x| in [2^-19, 2^19]: products of two such numbers are 0 or in [2^-38, 2^38]
+__device__ __forceinline__ bool in_range19(float x) {
+  const float m = fabsf(x);
+  return m == 0.0f || (m >= 0x1p-19f && m <= 0x1p19f);
+}
+// fdiv_core on a packed pair with the residual negated, r' = b q - a: the same quotient bit for
+// bit (round-to-nearest is sign-symmetric, and an exact-zero residual is +0 either way, which
+// leaves q unchanged), and for a = +-0 it keeps sign(a) without fdiv_core's copysign:
+// q0 = +-0, r' = +0, q = fma(-0, y, +-0) = +-0.  Both lanes round like the scalar fma.
+__device__ __forceinline__ pkf2 fdiv_core_pk(pkf2 a, pkf2 b, pkf2 y) {
+  const pkf2 q0 = a * y;
+  pkf2 r = __builtin_elementwise_fma(b, q0, -a);
+  const pkf2 q1 = __builtin_elementwise_fma(-r, y, q0);
+  r = __builtin_elementwise_fma(b, q1, -a);
+  return __builtin_elementwise_fma(-r, y, q1);
+}
 // f64 division with a hoisted reciprocal: hipcc's IEEE f64 sequence (v_div_scale, v_rcp_f64, two
 // Newton steps, q = n * y, r = fma(-d, q, n), v_div_fmas = fma(r, y, q), v_div_fixup) with the
 // scale / fixup steps dropped, which is exact while |n| and |d| lie in [2^-300, 2^300] (the
@@ -1319,6 +1344,23 @@ __device__ __forceinline__ double fdiv64(double n, const Recip64& r) {
   res = __builtin_copysign(res, q);  // +-0 / d keeps sign(n) * sign(d), as the IEEE quotient
   if (!(r.ok && (n == 0.0 || in_div_range64(n)))) res = fdiv64_ieee(n, r.d);
   return res;
+}
+// reciprocals of kernel-uniform divisors, moved to SGPRs (v_readfirstlane): VGPRs set the
+// occupancy of the throughput-bound sq16 kernel
+__device__ __forceinline__ float sgpr_f(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+__device__ __forceinline__ double sgpr_d(double x) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ Recip recip_u(float b) {
+  const Recip r = recip(b);
+  return Recip{b, sgpr_f(r.y), r.ok};
+}
+__device__ __forceinline__ Recip64 recip64_u(double d) {
+  const Recip64 r = recip64(d);
+  return Recip64{d, sgpr_d(r.y), r.ok};
 }
 // battery_rule (agent.py:138-153 + storage.py bookkeeping) with the divisions by the agent's
 // capacity, sqrt(efficiency) and 900 s through hoisted reciprocals; same op order, same results
@@ -1353,10 +1395,13 @@ __device__ __forceinline__ double battery_rule_r(double balance, double& soc, do
 //   * the final 16 x 16 proposal matrix is transposed through a swizzled LDS tile (4 x 16-B
 //     writes, 16 conflict-free 4-B reads);
 //   * the table is frozen for the episode: TD deltas go to the workgroup's LDS hash as before.
+#ifndef P2PMG_SQ16_OCC
+#define P2PMG_SQ16_OCC 4  // min waves per SIMD the register allocation must allow (LDS allows 4)
+#endif
 constexpr int kSq16Waves = 8;                        // waves per workgroup (one hash per 32 scenarios)
 constexpr int kTpStride = 16 * 16 + 16;              // floats per scenario tile (+16: bank offset)
 template <typename QT, int R1, bool TRAIN, bool BAT>
-__global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const EpisodeParams p) {
+__global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq16_kernel(const EpisodeParams p) {
   constexpr int N = 16, G = 16, SPW = kWave / G;
   __shared__ uint32_t hkey[kSqSlots];
   __shared__ unsigned long long hval[kSqSlots];
@@ -1371,7 +1416,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
   const int s_env = p.n_env == 1 ? 0 : (active ? s : 0);
   const int T = p.T;
   const size_t A = (size_t)p.A;
-  const KC k = pin_constants(p);
+  const KC k = scalar_constants(p);
   const Dims<true> D{k.nt, k.nT, k.nb, k.np};
   const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
   const QT* __restrict__ q = reinterpret_cast<const QT*>(p.q);
@@ -1389,7 +1434,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
   for (int m = 0; m < 4; ++m) cofs[m] = 4 * ((i >> 2) ^ m) + (i & 3);
 
   const float mi = active ? p.max_in[a] : 1.0f;
-  const Recip rmi = recip(mi), rmph = recip(k.mph), rmargin = recip(k.margin);
+  const Recip rmi = recip(mi), rmph = recip_u(k.mph), rmargin = recip_u(k.margin);
   const float4 lv = p.hp_lv[a];
   const bool margin_one = p.margin == 1.0f;
   double bcap = 0.0, soc = 0.0;
@@ -1398,7 +1443,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
   if constexpr (BAT) {
     bcap = p.bat_cap[a];
     soc = p.soc[a];
-    bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64(p.bat_sqrt_eff), recip64(900.0)};
+    bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64_u(p.bat_sqrt_eff), recip64_u(900.0)};
     rcap = recip64(bcap > 0.0 ? bcap : 1.0);
   }
   float tin = active ? p.t_in[a] : k.setpoint;
@@ -1477,6 +1522,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
       if (bcap > 0.0) out = (float)battery_rule_r((double)out, soc_r, bcap, rcap, bk);
     }
     const float ev0 = div_n<N>(out * 1.0f);
+    const bool ok_ev0 = in_range19(ev0);
 #pragma unroll
     for (int j = 0; j < N; ++j) row[j] = ev0;
     if constexpr (R1 == 2) {
@@ -1517,16 +1563,26 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
       const float ev = div_n<N>(out * 1.0f);
       const Recip rt = recip(tot == 0.0f ? 1.0f : tot);
       float num[N];
-      bool bad = !rt.ok;
 #pragma unroll
-      for (int j = 0; j < N; ++j) {
-        num[j] = out * fabsf(f[j]);
-        row[j] = fdiv_core(num[j], rt);
-        bad = bad || !fdiv_ok(num[j]);
-      }
-      if (bad) {
+      for (int j = 0; j < N; ++j) num[j] = out * fabsf(f[j]);
+      // One wave-uniform range guard instead of one per quotient: the column holds the group's
+      // round-0 values, each vouched for by its own lane (ok_ev0), so with out also in range
+      // every numerator is 0 or in [2^-38, 2^38] and the packed Newton quotient is exact.
+      if (__all(ok_ev0 && in_range19(out) && rt.ok)) {
+        const pkf2 y2 = {rt.y, rt.y}, b2 = {rt.b, rt.b};
 #pragma unroll
-        for (int j = 0; j < N; ++j) row[j] = fdiv_ieee(num[j], rt.b);
+        for (int j = 0; j < N; j += 2) {
+          const pkf2 q2 = fdiv_core_pk(pkf2{num[j], num[j + 1]}, b2, y2);
+          row[j] = q2.x;
+          row[j + 1] = q2.y;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) row[j] = fdiv_b(num[j], rt);
+        if (!rt.ok) {
+#pragma unroll
+          for (int j = 0; j < N; ++j) row[j] = fdiv_ieee(num[j], rt.b);
+        }
       }
 #pragma unroll
       for (int j = 0; j < N; ++j) row[j] = (tot == 0.0f) ? ev : row[j];
@@ -1551,16 +1607,24 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
 #pragma unroll
     for (int j = 0; j < N; ++j) col[j] = tp[j * 16 + cofs[j & 3]];
     wave_lds_fence();
-    float g = 0.0f, pp = 0.0f;
+    // (g, pp) as one packed pair: g += pij - ex and pp += ex in one v_pk_add_f32 per j, the
+    // differences two j at a time (each lane of a packed op rounds like the scalar op)
+    pkf2 gp = {0.0f, 0.0f};
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const float pij = row[j], pji = col[j];
-      const float mn = __builtin_amdgcn_fmed3f(fabsf(pij), fabsf(pji), -__builtin_inff());
-      const bool opp = ((__float_as_uint(pij) ^ __float_as_uint(pji)) >> 31) != 0u;
-      const float ex = opp ? __builtin_copysignf(mn, pij) : 0.0f;
-      g = g + (pij - ex);
-      pp = pp + ex;
+    for (int j = 0; j < N; j += 2) {
+      float ex[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float pij = row[j + u], pji = col[j + u];
+        const float mn = __builtin_amdgcn_fmed3f(fabsf(pij), fabsf(pji), -__builtin_inff());
+        const bool opp = ((__float_as_uint(pij) ^ __float_as_uint(pji)) >> 31) != 0u;
+        ex[u] = opp ? __builtin_copysignf(mn, pij) : 0.0f;
+      }
+      const pkf2 d = pkf2{row[j], row[j + 1]} - pkf2{ex[0], ex[1]};
+      gp = gp + pkf2{d.x, ex[0]};
+      gp = gp + pkf2{d.y, ex[1]};
     }
+    const float g = gp.x, pp = gp.y;
     float cost = (g >= 0.0f) ? g * e0.buy : g * e0.inj;
     cost = cost + pp * e0.p2p;
     cost = fdiv_b(cost * k.slot, rmph);
@@ -1573,8 +1637,11 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
       if (active) {
         const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
         const double d = k.alpha * (((double)rw + k.gamma * (double)max3(rowN)) - (double)qsa);
-        lds_add_by_key(hkey, hval, (st.strip + (uint32_t)ip) * kQPad + (uint32_t)act, __double2ll_rn(d * kDeltaScale),
-                       dbase);
+        const long long dv = __double2ll_rn(d * kDeltaScale);
+#if P2PMG_SQ_ABL == 1
+        if (dv == 0x7123456789LL)  // timing-only ablation: no hash insert (never true in practice)
+#endif
+        lds_add_by_key(hkey, hval, (st.strip + (uint32_t)ip) * kQPad + (uint32_t)act, dv, dbase);
       }
     }
     if (narrow) {
@@ -1598,7 +1665,12 @@ __global__ __launch_bounds__(kWave * kSq16Waves) void episode_sq16_kernel(const 
     wave_lds_fence();
     ep_sum = ep_sum + div_n<N>(msum);
     if constexpr (TRAIN) {
-      if (t % kSqFlushSteps == kSqFlushSteps - 1 || t + 1 == T) lds_hash_flush(hkey, hval, dbase, kSq16Waves * kWave);
+#if P2PMG_SQ_ABL == 2
+      if (t + 1 == T)  // timing-only ablation: one flush at the end
+#else
+      if (t % kSqFlushSteps == kSqFlushSteps - 1 || t + 1 == T)
+#endif
+        lds_hash_flush(hkey, hval, dbase, kSq16Waves * kWave);
     }
 
     tin = tin1;

@@ -1,6 +1,6 @@
 """Timing probe of episode_sq16_kernel variants at the configs[2] shape (N=16, shared table, battery).
 Prints median episode-kernel ms per variant (HIP events stamped by the dispatch)."""
-import json, sys
+import json, sys, time
 import numpy as np
 sys.path.insert(0, '.')
 from p2pmicrogrid_amd.dataset import scenario_batch
@@ -18,16 +18,22 @@ variants = [("train inkernel", dict(mode="train", philox="auto", record=("reward
             ("train norecord", dict(mode="train", philox="auto", record=())),
             ("greedy", dict(mode="greedy", philox="auto", record=("reward", "cost"))),
             ("train general", dict(mode="train", philox="auto", record=("reward", "cost"), kernel="general"))]
+only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
 for name, kw in variants:
+    if only and name not in only:
+        continue
     mode = kw.pop("mode")
     for k in range(2):
         e.run_episode(mode, "philox", episode=k, epsilon=0.5, **kw)
         e.apply_q_delta()
     e.sync(); e.reset_kernel_times()
+    t0 = time.perf_counter()
     for k in range(4):
         e.run_episode(mode, "philox", episode=3 + k, epsilon=0.5, **kw)
         e.apply_q_delta()
+    e.sync()
+    res[name + " wall"] = (time.perf_counter() - t0) / 4 * 1e3
     res[name] = float(np.median(e.kernel_times()))
     res[name + " kernel"] = e.last_kernel()
-    print(name, res[name], flush=True)
+    print(name, res[name], "wall/episode", res[name + " wall"], flush=True)
 print(json.dumps(res))
