@@ -176,6 +176,13 @@ int p2pmg_get_q(p2pmg_ctx* ctx, int first_agent, int count, void* host, int host
 /* the hot path */
 int p2pmg_run_episode(p2pmg_ctx* ctx, const p2pmg_episode_args* args);
 int p2pmg_get_record(p2pmg_ctx* ctx, int which, void* host);   /* one P2PMG_REC_* bit */
+/* RuleAgent community run (get_rule_based_community community.py:237-238 -> run() community.py:95-123,
+ * RuleAgent agent.py:106-136): hysteresis heat pump at the heat pump's max power (level 2 of
+ * p2pmg_set_hp_levels), no policy, R = 0.  Records: COST, GRID, P2P, TEMP, ACTION (0 off / 2 on). */
+int p2pmg_run_rule_episode(p2pmg_ctx* ctx, int record);
+/* HeatPump.power of each RuleAgent (0 or 1; persists across runs like the reference's): [A] */
+int p2pmg_set_hp_state(p2pmg_ctx* ctx, const float* on);
+int p2pmg_get_hp_state(p2pmg_ctx* ctx, float* on);
 int p2pmg_get_episode_reward(p2pmg_ctx* ctx, float* host);     /* [S]: sum_t mean_i r (community.py:179) */
 int p2pmg_last_kernel_ms(p2pmg_ctx* ctx, float* ms);           /* HIP-event time of the last episode kernel */
 /* HIP-event durations (ms) of the episode kernels launched since the last reset, oldest first

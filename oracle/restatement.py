@@ -184,6 +184,27 @@ def assign_powers(P):
     return p_grid, p_p2p
 
 
+def rule_assign_powers(Pv):
+    """CommunityMicrogrid._assign_powers (community.py:45-54) on a RuleAgent community's stack.
+
+    RuleAgent.take_decision returns its net power as a (1,) tensor (agent.py:111-128), so the
+    stacked P is (N, 1): TF broadcasts P (N,1) against P^T (1,N) inside ``tf.where`` and the
+    subtraction, giving ex[i,j] = sign(P_i) min(|P_i|, |P_j|) on differing signs and
+    p_grid[i] = sum_j (P_i - ex[i,j]) over all N columns (a reference quirk: N copies of P_i).
+    Pv: (..., N) f32.
+    """
+    Pv = np.asarray(Pv, dtype=F32)
+    P = Pv[..., :, None]
+    PT = Pv[..., None, :]
+    cond = sign(P) != sign(PT)
+    pm = np.where(cond, P, F32(0)).astype(F32)
+    apm = np.abs(pm)
+    ex = (sign(pm) * np.minimum(apm, np.swapaxes(apm, -1, -2))).astype(F32)
+    p_grid = seq_sum((P - ex).astype(F32))
+    p_p2p = seq_sum(ex)
+    return p_grid, p_p2p
+
+
 def compute_costs(g, pp, buy, inj, p2p, p: OracleParams = OracleParams()):
     """CommunityMicrogrid._compute_costs (community.py:56-65)."""
     g = np.asarray(g, dtype=F32)
@@ -320,6 +341,38 @@ class OracleBatch:
         q0 = self.q[0]
         q0[nz] = (q0[nz].astype(np.float64) + self.q_delta[nz].astype(np.float64) * (1.0 / DELTA_SCALE)).astype(q0.dtype)
         self.q_delta[:] = 0
+
+    def run_rule_episode(self, hp_on: np.ndarray) -> Dict:
+        """CommunityMicrogrid.run (community.py:95-123) of a RuleAgent community
+        (get_rule_based_community, community.py:237-238; RuleAgent agent.py:106-136), R = 0.
+
+        Per step: the hysteresis heating rule on the pre-update T_in (agent.py:130-136: on at
+        T_in <= setpoint - 1, off at T_in >= setpoint + 1, else unchanged), net power
+        (load - pv) + hp (agent.py:119-128), the (N, 1)-broadcast market, costs, then the RC step
+        with hp (HPHeating.step heating.py:138-143).  hp_on: [S, N] 0/1 state of HeatPump.power,
+        updated in place (it persists across runs: HPHeating.reset does not touch it)."""
+        p = self.params
+        S, N, T = self.S, self.N, self.T
+        hpmax = self.hp_levels[:, :, 2]
+        tr = {k: [] for k in ("grid", "p2p", "cost", "t_in", "hp", "on")}
+        for t in range(T):
+            tout = self._env(self.env_tout, t)
+            hp_on = np.where(self.t_in <= F32(p.lower), 1, np.where(self.t_in >= F32(p.upper), 0, hp_on))
+            hp = (hp_on.astype(F32) * hpmax).astype(F32)  # HPHeating.power: hp.power * max_power
+            Pv = ((self.load_w[:, :, t] - self.pv_w[:, :, t]) + hp).astype(F32)
+            g, pp = rule_assign_powers(Pv)
+            cost = compute_costs(g, pp, self._env(self.buy, t)[:, None], self._env(self.inj, t)[:, None],
+                                 self._env(self.p2p, t)[:, None], p)
+            tr["grid"].append(g)
+            tr["p2p"].append(pp)
+            tr["cost"].append(cost)
+            tr["t_in"].append(self.t_in.copy())
+            tr["hp"].append(hp)
+            tr["on"].append(hp_on.copy())
+            self.t_in, self.t_m = temperature_step(tout[:, None], self.t_in, self.t_m, hp, p)
+        out = {k: np.stack(v) for k, v in tr.items()}
+        out["hp_on"] = hp_on
+        return out
 
     def _env(self, arr, t):
         return arr[:, t] if arr.shape[0] == self.S else np.broadcast_to(arr[0, t], (self.S,))

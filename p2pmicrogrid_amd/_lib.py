@@ -33,7 +33,8 @@ EXPORTS = [
     "p2pmg_state_indices", "p2pmg_replay_decode", "p2pmg_device_count", "p2pmg_kernel_times",
     "p2pmg_reset_kernel_times", "p2pmg_q_calls", "p2pmg_set_hp_levels", "p2pmg_set_battery", "p2pmg_get_soc",
     "p2pmg_battery_seq", "p2pmg_apply_q_delta", "p2pmg_get_q_delta", "p2pmg_set_q_delta", "p2pmg_comm_unique_id", "p2pmg_comm_init",
-    "p2pmg_allreduce_q_delta", "p2pmg_comm_destroy",
+    "p2pmg_allreduce_q_delta", "p2pmg_comm_destroy", "p2pmg_run_rule_episode", "p2pmg_set_hp_state",
+    "p2pmg_get_hp_state",
     "p2pmg_dqn_config_default", "p2pmg_dqn_setup", "p2pmg_dqn_set_weights", "p2pmg_dqn_get_weights",
     "p2pmg_dqn_set_step", "p2pmg_dqn_get_step", "p2pmg_dqn_set_samples", "p2pmg_dqn_get_buffer",
     "p2pmg_dqn_set_buffer", "p2pmg_dqn_forward", "p2pmg_dqn_train_batch",
@@ -113,6 +114,9 @@ def _declare(lib):
         "p2pmg_reset_kernel_times": ([vp], i32),
         "p2pmg_q_calls": ([vp, i32, vp, vp, vp, vp, vp, i32, vp, vp], i32),
         "p2pmg_set_hp_levels": ([vp, fp], i32),
+        "p2pmg_run_rule_episode": ([vp, i32], i32),
+        "p2pmg_set_hp_state": ([vp, fp], i32),
+        "p2pmg_get_hp_state": ([vp, fp], i32),
         "p2pmg_set_battery": ([vp, vp, C.c_double, C.c_double, C.c_double, vp], i32),
         "p2pmg_get_soc": ([vp, vp], i32),
         "p2pmg_battery_seq": ([vp, i32, i32, vp, vp, vp, vp, vp, C.c_double, C.c_double, C.c_double], i32),

@@ -107,6 +107,33 @@ class ActingAgent(Agent, ABC):
         self.reset()
 
 
+class RuleAgent(ActingAgent):
+    """Rule-based baseline (agent.py:106-153): the heat pump follows a hysteresis on the indoor
+    temperature (on at T_in <= setpoint - 1, off at T_in >= setpoint + 1), the net power is
+    (load - pv) + heat-pump power, and nothing is learned.  Inside a CommunityMicrogrid
+    (``get_rule_based_community``) a whole run is one device launch (rule_episode_kernel)."""
+
+    def __call__(self, *args, **kwargs):
+        raise NotImplementedError(_FUSED)
+
+    def take_decision(self, *args, **kwargs):
+        raise NotImplementedError(_FUSED)
+
+    def _update_storage(self, balance: float) -> float:
+        """agent.py:138-153: greedy battery rule on the net balance (W); returns the remainder.
+        The reference never calls it from a community; kept for scripts that do."""
+        energy = balance * setup.SECONDS_PER_MINUTE * setup.TIME_SLOT
+        if balance > 0 and self.storage.available_energy > 0:
+            to_extract = min(energy, self.storage.available_energy)
+            self.storage.discharge(self.storage.to_soc(to_extract))
+            balance -= to_extract / (setup.SECONDS_PER_MINUTE * setup.TIME_SLOT)
+        elif balance < 0 and not self.storage.is_full:
+            to_store = min(-energy, self.storage.available_space)
+            self.storage.charge(self.storage.to_soc(to_store))
+            balance += to_store / (setup.SECONDS_PER_MINUTE * setup.TIME_SLOT)
+        return balance
+
+
 class RLAgent(ActingAgent):
 
     def __init__(self, actor, *args, **kwargs):
@@ -175,4 +202,6 @@ def agent_kind(agent) -> Optional[str]:
         return "tabular"
     if isinstance(agent, DQNAgent):
         return "dqn"
+    if isinstance(agent, RuleAgent):
+        return "rule"
     return None

@@ -19,7 +19,7 @@ import numpy as np
 
 from . import dataset as ds
 from . import setup
-from .agent import ActingAgent, Agent, DQNAgent, GridAgent, QAgent, agent_kind
+from .agent import ActingAgent, Agent, DQNAgent, GridAgent, QAgent, RuleAgent, agent_kind
 from .engine import DeviceCommunityBatch, price_table
 from .environment import env
 from .heating import HeatPump, HPHeating
@@ -49,6 +49,7 @@ class CommunityMicrogrid:
         if len(kinds) != 1 or None in kinds:
             raise ValueError(f"a community needs agents of one learner kind, got {kinds}")
         self._dqn = kinds == {"dqn"}
+        self._rule = kinds == {"rule"}
 
     # ------------------------------------------------------------ device state
     def _new_dqn_engine(self, T, N):
@@ -83,6 +84,8 @@ class CommunityMicrogrid:
                 tables = None
             self._engine = DeviceCommunityBatch(1, N, self._rounds, T, q_dtype=self._q_dtype, device=self._device)
             for i, a in enumerate(self.agents):
+                if self._rule:  # no policy to bind
+                    continue
                 if tables is None:
                     a.actor.bind(self._engine, i)
                 else:
@@ -122,6 +125,9 @@ class CommunityMicrogrid:
         (the loss is 0 for tabular agents, agent.py:298)."""
         if self._dqn:
             return self._train_episode_dqn()
+        if self._rule:  # community.py:160-171 calls agent.get_reward / agent.train, which RuleAgent lacks
+            raise AttributeError("'RuleAgent' object has no attribute 'get_reward': rule-based communities "
+                                 "only run() (agent.py:106-153)")
         eng = self._ensure_engine()
         T, N = eng.T, eng.N
         self._push_temperatures(eng)
@@ -138,6 +144,8 @@ class CommunityMicrogrid:
 
     def run(self) -> Tuple[np.ndarray, np.ndarray]:
         """community.py:95-123: greedy rollout; returns (grid + p2p power [T, N], costs [T, N])."""
+        if self._rule:
+            return self._run_rule()
         eng = self._ensure_engine()
         T = eng.T
         self._push_temperatures(eng)
@@ -151,6 +159,31 @@ class CommunityMicrogrid:
             a.heating._history = [float(x) for x in hist[:, i]]
             a.heating._power_history = list(self.decisions[:, -1, i])
             a.heating.set_state(t_in[0, i], t_m[0, i])
+        power = (r["grid"][:, 0, :] + r["p2p"][:, 0, :]).astype(F32)
+        return power, r["cost"][:, 0, :]
+
+    def _run_rule(self) -> Tuple[np.ndarray, np.ndarray]:
+        """run() of a RuleAgent community: one rule_episode_kernel launch (R = 0)."""
+        if self._rounds != 0:
+            raise ValueError("RuleAgent communities run with rounds = 0: with more rounds the reference's "
+                             "tensor_diag_part on the (N, 1) proposal stack fails (community.py:76)")
+        eng = self._ensure_engine()
+        self._push_temperatures(eng)
+        levels = np.array([[0.0, 0.5, 1.0]], F32) * np.array([[a.heating.hp.max_power] for a in self.agents], F32)
+        eng.set_hp_levels(levels[None])
+        eng.set_hp_state(np.array([float(np.asarray(a.heating.hp.power).reshape(-1)[0]) for a in self.agents], F32)[None])
+        rec = ("grid", "p2p", "cost", "t_in", "action")
+        eng.run_rule_episode(record=rec)
+        r = eng.get_records(rec)
+        self._pull_records(eng, eng.T)
+        t_in, t_m = eng.get_temperatures()
+        on = eng.get_hp_state()[0]
+        hist = r["t_in"][:, 0, :] if r["t_in"].ndim == 3 else r["t_in"]
+        for i, a in enumerate(self.agents):
+            a.heating._history = [float(x) for x in hist[:, i]]
+            a.heating._power_history = list(self.decisions[:, -1, i])
+            a.heating.set_state(t_in[0, i], t_m[0, i])
+            a.heating.hp.power = float(on[i])
         power = (r["grid"][:, 0, :] + r["p2p"][:, 0, :]).astype(F32)
         return power, r["cost"][:, 0, :]
 
@@ -232,6 +265,12 @@ def get_community(agent_constructor: Callable[..., ActingAgent], n_agents: int,
                                         max_out=-(max_power + safety * 1e3)))
     env.setup(ds.dataframe_to_dataset(env_df))
     return CommunityMicrogrid(timeline, agents, setup.rounds if rounds_ is None else rounds_)
+
+
+def get_rule_based_community(n_agents: int, homogeneous: bool) -> CommunityMicrogrid:
+    """community.py:237-238, with rounds = 0: a RuleAgent ignores the proposals, and with more
+    rounds the reference's run() fails on the (N, 1) proposal stack (tensor_diag_part)."""
+    return get_community(RuleAgent, n_agents, homogeneous=homogeneous, rounds_=0)
 
 
 def get_rl_based_community(n_agents: int, homogeneous: bool) -> CommunityMicrogrid:

@@ -120,6 +120,8 @@ hipError_t launch_step_prepass(const EpisodeParams& p, const PrepOut& o, hipStre
 // ev0 / ev1: timing events stamped by the dispatch (hipExtLaunchKernel)
 hipError_t launch_episode_fast(const EpisodeParams& p, const uint2* pre, void* recs, int q_dtype, int spw,
                                const PrepOut* next, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
+// RuleAgent community run (R = 0): rule_episode_kernel; hp_on [A] hysteresis state in/out
+hipError_t launch_rule_episode(const EpisodeParams& p, float* hp_on, hipStream_t stream);
 // shared table, N = 16, R <= 1 (configs[2]): episode_sq16_kernel; records packed like the fast path
 hipError_t launch_episode_sq16(const EpisodeParams& p, int q_dtype, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
 constexpr size_t kFastRecBytes = 32;  // one packed record row per agent-step (FastRec)

@@ -1718,6 +1718,81 @@ hipError_t launch_sq16_q(const EpisodeParams& p, hipEvent_t ev0, hipEvent_t ev1,
   return hipGetLastError();
 }
 
+// ----------------------------------------------------------------- RuleAgent communities
+// CommunityMicrogrid.run (community.py:95-123) of get_rule_based_community (community.py:237-238):
+// every agent is a RuleAgent (agent.py:106-136), so there is no policy and no exchange round.
+// Per step: the hysteresis rule on the pre-update T_in (on at T_in <= setpoint - 1, off at
+// T_in >= setpoint + 1, else unchanged; agent.py:130-136), net power (load - pv) + hp
+// (agent.py:119-128), the market on the (N, 1) stack (TF broadcasts it against its transpose:
+// ex_ij = sign(P_i) min(|P_i|, |P_j|) on differing signs, p_grid_i = sum_j (P_i - ex_ij),
+// community.py:45-54), costs (community.py:56-65), then HPHeating.step (heating.py:138-143).
+// One lane per agent, G lanes per scenario, the group's P through LDS; hp_on persists.
+template <int G>
+__global__ __launch_bounds__(kWave) void rule_episode_kernel(const EpisodeParams p, float* __restrict__ hp_on) {
+  constexpr int SPW = kWave / G;
+  __shared__ float shP[kWave];
+  const int lane = (int)threadIdx.x;
+  const int sl = lane / G, i = lane % G;
+  const int N = p.N;
+  const int s = (int)blockIdx.x * SPW + sl;
+  const bool active = i < N && s < p.S;
+  const int a = active ? s * N + i : 0;
+  const int s_env = p.n_env == 1 ? 0 : (s < p.S ? s : 0);
+  const size_t A = (size_t)p.A;
+  const KC k = scalar_constants(p);
+  const Recip rmph = recip(k.mph);
+  const float hpmax = p.hp_lv[a].z;  // HeatPump.max_power (hp.power in {0, 1})
+  float on = active ? hp_on[a] : 0.0f;
+  float tin = active ? p.t_in[a] : k.setpoint;
+  float tm = active ? p.t_m[a] : k.setpoint;
+  const float* envb = p.env + (size_t)s_env * kEnvStride;
+  const size_t env_step = (size_t)p.n_env * kEnvStride;
+  const uint32_t rec = (uint32_t)p.record;
+  for (int t = 0; t < p.T; ++t) {
+    const EnvRow e = load_env(envb + (size_t)t * env_step);
+    const float2 f = p.prof[(size_t)t * A + a];
+    on = tin <= k.lower ? 1.0f : (tin >= k.upper ? 0.0f : on);
+    const float hp = on * hpmax;
+    const float P = (f.x - f.y) + hp;
+    shP[lane] = P;
+    wave_lds_fence();
+    float g = 0.0f, pp = 0.0f;
+    for (int j = 0; j < N; ++j) {
+      const float pj = shP[sl * G + j];
+      const float mn = fminf(fabsf(P), fabsf(pj));
+      const bool opp = ((__float_as_uint(P) ^ __float_as_uint(pj)) >> 31) != 0u;
+      const float ex = opp ? __builtin_copysignf(mn, P) : 0.0f;
+      g = g + (P - ex);
+      pp = pp + ex;
+    }
+    wave_lds_fence();
+    float cost = (g >= 0.0f) ? g * e.buy : g * e.inj;
+    cost = cost + pp * e.p2p;
+    cost = fdiv_b(cost * k.slot, rmph);
+    cost = cost * k.kilo;
+    if (active) {
+      const size_t tA = (size_t)t * A + a;
+      if (rec & 2u) p.rec_cost[tA] = cost;
+      if (rec & 4u) p.rec_grid[tA] = g;
+      if (rec & 8u) p.rec_p2p[tA] = pp;
+      if (rec & 16u) p.rec_tin[tA] = tin;
+      if (rec & 32u) p.rec_action[tA] = on != 0.0f ? 2 : 0;  // action 2 = 1.0 x max_power
+    }
+    rc_update(k, e.t_out, hp, tin, tm);
+  }
+  if (active) {
+    p.t_in[a] = tin;
+    p.t_m[a] = tm;
+    hp_on[a] = on;
+  }
+}
+
+template <int G>
+void launch_rule_g(const EpisodeParams& p, float* hp_on, hipStream_t st) {
+  constexpr int SPW = kWave / G;
+  hipLaunchKernelGGL(rule_episode_kernel<G>, dim3((p.S + SPW - 1) / SPW), dim3(kWave), 0, st, p, hp_on);
+}
+
 template <int N, typename QT, bool SQ>
 void launch_nq(const EpisodeParams& p, hipStream_t st) {
   constexpr int SPW = kWave / pow2ceil(N);
@@ -1893,6 +1968,19 @@ hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void*
 
 hipError_t launch_episode_sq16(const EpisodeParams& p, int q_dtype, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream) {
   return q_dtype == 0 ? launch_sq16_q<double>(p, ev0, ev1, stream) : launch_sq16_q<float>(p, ev0, ev1, stream);
+}
+
+hipError_t launch_rule_episode(const EpisodeParams& p, float* hp_on, hipStream_t stream) {
+  const int n = p.N;
+  if (n <= 1) launch_rule_g<1>(p, hp_on, stream);
+  else if (n <= 2) launch_rule_g<2>(p, hp_on, stream);
+  else if (n <= 4) launch_rule_g<4>(p, hp_on, stream);
+  else if (n <= 8) launch_rule_g<8>(p, hp_on, stream);
+  else if (n <= 16) launch_rule_g<16>(p, hp_on, stream);
+  else if (n <= 32) launch_rule_g<32>(p, hp_on, stream);
+  else if (n <= 64) launch_rule_g<64>(p, hp_on, stream);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
 }
 
 hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream) {

@@ -68,6 +68,7 @@ struct p2pmg_ctx {
   uint8_t* rec_action = nullptr;
   int32_t* rec_index = nullptr;
   float4* hp_lv = nullptr;     // [A] per-agent heat-pump levels
+  float* hp_on = nullptr;      // [A] RuleAgent heat-pump state (lazily allocated, starts off)
   double* soc = nullptr;       // [A]
   double* bat_cap = nullptr;   // [A]
   bool battery = false;
@@ -326,6 +327,7 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   dfree(c->rec_action);
   dfree(c->rec_index);
   dfree(c->hp_lv);
+  dfree(c->hp_on);
   dfree(c->soc);
   dfree(c->bat_cap);
   dfree(c->qdelta);
@@ -722,6 +724,62 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     HIP_TRY(c, p2pmg::launch_t0_philox(c->A, c->t_in, c->t_m, p.seed_lo, p.seed_hi, args->episode + 1, off,
                                        g.setpoint, args->reset_sigma, c->stream));
   }
+  c->timed = true;
+  c->n_timed++;
+  return P2PMG_OK;
+}
+
+static int ensure_hp_on(p2pmg_ctx* c) {
+  if (c->hp_on) return P2PMG_OK;
+  HIP_TRY(c, dmalloc(&c->hp_on, (size_t)c->A));
+  HIP_TRY(c, hipMemsetAsync(c->hp_on, 0, (size_t)c->A * sizeof(float), c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_set_hp_state(p2pmg_ctx* c, const float* on) {
+  if (!c || !on) return P2PMG_E_INVALID;
+  int rc = ensure_hp_on(c);
+  if (rc != P2PMG_OK) return rc;
+  HIP_TRY(c, hipMemcpyAsync(c->hp_on, on, (size_t)c->A * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_get_hp_state(p2pmg_ctx* c, float* on) {
+  if (!c || !on) return P2PMG_E_INVALID;
+  int rc = ensure_hp_on(c);
+  if (rc != P2PMG_OK) return rc;
+  HIP_TRY(c, hipMemcpyAsync(on, c->hp_on, (size_t)c->A * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_run_rule_episode(p2pmg_ctx* c, int record) {
+  if (!c) return P2PMG_E_INVALID;
+  if (c->dqn) return fail(c, P2PMG_E_STATE, "run_rule_episode: DQN context");
+  if (!c->have_env || !c->have_prof || !c->have_params)
+    return fail(c, P2PMG_E_STATE, "run_rule_episode: env, profiles and agent params must be set first");
+  if (c->R != 0)  // the reference's tensor_diag_part on the (N, 1) stack fails for rounds > 0
+    return fail(c, P2PMG_E_INVALID, "run_rule_episode: RuleAgent communities run with rounds = 0");
+  if (c->N > 64) return fail(c, P2PMG_E_INVALID, "run_rule_episode: N <= 64");
+  const int rec = record & (P2PMG_REC_COST | P2PMG_REC_GRID | P2PMG_REC_P2P | P2PMG_REC_TEMP | P2PMG_REC_ACTION);
+  int rc = ensure_records(c, rec);
+  if (rc == P2PMG_OK) rc = ensure_hp_on(c);
+  if (rc != P2PMG_OK) return rc;
+  p2pmg_episode_args args{};
+  args.mode = P2PMG_MODE_GREEDY;
+  args.record = rec;
+  EpisodeParams p = episode_params(c, &args);
+  if (c->ring.empty()) {
+    c->ring.assign(2 * p2pmg_ctx::kRing, nullptr);
+    for (auto& ev : c->ring) HIP_TRY(c, hipEventCreate(&ev));
+  }
+  const int slot = (int)(c->n_timed % p2pmg_ctx::kRing);
+  HIP_TRY(c, hipEventRecord(c->ring[2 * slot], c->stream));
+  HIP_TRY(c, p2pmg::launch_rule_episode(p, c->hp_on, c->stream));
+  HIP_TRY(c, hipEventRecord(c->ring[2 * slot + 1], c->stream));
+  c->rec_fast_mask = 0;
+  c->last_kernel = "rule_episode_kernel<" + std::to_string(c->N) + ">";
   c->timed = true;
   c->n_timed++;
   return P2PMG_OK;

@@ -235,6 +235,25 @@ class DeviceCommunityBatch:
         self._chk(self.L.p2pmg_run_episode(self._ctx, C.byref(args)), "run_episode")
         self._recorded = mask
 
+    def run_rule_episode(self, record: Sequence[str] = ()):
+        """CommunityMicrogrid.run of a RuleAgent community (community.py:95-123, 237-238; agent.py:106-136):
+        hysteresis heat pumps, no policy, R = 0.  Records: cost, grid, p2p, t_in, action (0 off, 2 on)."""
+        mask = 0
+        for r in record:
+            mask |= _lib.REC[r]
+        self._chk(self.L.p2pmg_run_rule_episode(self._ctx, mask), "run_rule_episode")
+        self._recorded = mask
+
+    def set_hp_state(self, on):
+        """RuleAgent HeatPump.power per agent (0/1), [S, N]."""
+        a = np.ascontiguousarray(np.asarray(on, dtype=F32).reshape(self.A))
+        self._chk(self.L.p2pmg_set_hp_state(self._ctx, a), "set_hp_state")
+
+    def get_hp_state(self) -> np.ndarray:
+        out = np.empty(self.A, F32)
+        self._chk(self.L.p2pmg_get_hp_state(self._ctx, out), "get_hp_state")
+        return out.reshape(self.S, self.N)
+
     def last_kernel(self) -> str:
         """Name of the kernel the last episode launch ran (fast or general path)."""
         return (self.L.p2pmg_last_kernel(self._ctx) or b"").decode()

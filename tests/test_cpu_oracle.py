@@ -149,3 +149,44 @@ def test_battery_rule_matches_reference_storage():
                                np.sqrt(float(d["efficiency"])))
         assert ob == d["out_bal"][k] and soc == d["soc"][k], k
     assert np.all(d["soc"] >= 0.1 - 1e-12) and np.all(d["soc"] <= 0.9 + 1e-12)
+
+
+def test_rule_community_market_broadcast_quirk():
+    """RuleAgent's (1,) outputs stack to an (N, 1) P; community.py:45-54 broadcasts it against its
+    transpose (worked by hand from TF's broadcasting rules): p_grid_i = sum_j (P_i - ex_ij)."""
+    from oracle.restatement import rule_assign_powers
+    g, pp = rule_assign_powers(np.array([1000.0, -2000.0], np.float32))
+    assert np.array_equal(pp, np.array([1000.0, -1000.0], np.float32))
+    assert np.array_equal(g, np.array([1000.0, -3000.0], np.float32))  # (1000-0)+(1000-1000); (-2000+1000)+(-2000-0)
+    g, pp = rule_assign_powers(np.array([[500.0], [-200.0]], np.float32).T)  # one scenario, N = 2
+    assert np.array_equal(pp, np.array([[200.0, -200.0]], np.float32))
+    g1, pp1 = rule_assign_powers(np.array([700.0], np.float32))  # N = 1: grid = P
+    assert g1[0] == np.float32(700.0) and pp1[0] == 0
+
+
+def test_rule_oracle_hysteresis():
+    from oracle.restatement import OracleBatch
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    S, N, T = 3, 2, 96
+    inp = scenario_batch(S, N, T)
+    ob = OracleBatch(S=S, N=N, R=0, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in,
+                     env_time=inp.time[None], env_tout=inp.t_out)
+    ob.t_in = np.full((S, N), np.float32(19.5))
+    ob.t_m = np.full((S, N), np.float32(19.5))
+    out = ob.run_rule_episode(np.zeros((S, N), np.int64))
+    assert out["on"][0].all() and out["hp"][0].max() == np.float32(3000.0)  # cold start: on
+    on, tin = out["on"], out["t_in"]
+    for t in range(1, T):  # hysteresis: switches only at the band edges
+        sw_on = (on[t] == 1) & (on[t - 1] == 0)
+        sw_off = (on[t] == 0) & (on[t - 1] == 1)
+        assert (tin[t][sw_on] <= np.float32(20.0)).all() and (tin[t][sw_off] >= np.float32(22.0)).all()
+
+
+def test_rule_community_api_only_runs():
+    import pytest
+    from p2pmicrogrid_amd.community import get_rule_based_community
+    np.random.seed(42)
+    com = get_rule_based_community(2, homogeneous=False)
+    assert com._rounds == 0 and {type(a).__name__ for a in com.agents} == {"RuleAgent"}
+    with pytest.raises(AttributeError):
+        com.train_episode()
