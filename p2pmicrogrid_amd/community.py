@@ -17,6 +17,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 
+from . import database as db
 from . import dataset as ds
 from . import setup
 from .agent import ActingAgent, Agent, DQNAgent, GridAgent, QAgent, RuleAgent, agent_kind
@@ -291,9 +292,10 @@ def setting_name(nr_agents=None, rounds=None, homogeneous=None) -> str:
 
 
 def main(load_agents: bool = False, episodes: Optional[int] = None, save: bool = True,
-         verbose: bool = True) -> Dict[str, Any]:
-    """community.py:248-321 training loop (DB logging and plotting out of scope): epsilon decay
-    after episodes 0, 50, ...; checkpoints every ``save_episodes`` and at the end."""
+         verbose: bool = True, con=None) -> Dict[str, Any]:
+    """community.py:248-321 training loop: epsilon decay after episodes 0, 50, ...; the running
+    means go to ``training_progress`` when a connection is given (db.log_training_progress);
+    checkpoints every ``save_episodes`` and at the end.  Plotting is out of scope."""
     setting = setting_name()
     community = get_rl_based_community(setup.nr_agents, homogeneous=setup.homogeneous)
     if load_agents:
@@ -317,18 +319,46 @@ def main(load_agents: bool = False, episodes: Optional[int] = None, save: bool =
                       f'Average error: {statistics.mean(errors_q):.3f}')
             for agent in community.agents:
                 agent.actor.decay_exploration()
+            db.log_training_progress(con, setting, setup.implementation, episode, statistics.mean(rewards_q),
+                                     statistics.mean(errors_q))
         if save and (episode + 1) % setup.save_episodes == 0:
             for agent in community.agents:
                 agent.save_to_file(setting, setup.implementation)
+    if history:
+        db.log_training_progress(con, setting, setup.implementation, last - 1, statistics.mean(rewards_q),
+                                 statistics.mean(errors_q))
     if save:
         for agent in community.agents:
             agent.save_to_file(setting, setup.implementation)
     return {"community": community, "rewards": history, "train_time": time.time() - t0}
 
 
-def load_and_run(is_testing: bool = False) -> Dict[int, Dict[str, np.ndarray]]:
-    """community.py:364-412 without the DB sink: greedy evaluation per test/validation day from
-    the saved tables, a fresh start each day; returns per-day power, cost and decisions."""
+def save_community_results(con, is_testing: bool, setting: str, day: int, community: CommunityMicrogrid,
+                           cost: np.ndarray) -> None:
+    """community.py:333-353: one test/validation row per agent-step (time, load, pv, T_in, heat-pump
+    power, cost) and, for test runs, the heat-pump decision of every negotiation round."""
+    time_f, _ = env.arrays()
+    T = len(time_f)
+    times = [float(x) for x in time_f]
+    days = [int(day)] * T
+    impl = setup.implementation
+    for i, agent in enumerate(community.agents):
+        row = (agent.load_series(T), agent.pv.series(T), agent.heating.get_history(),
+               agent.heating._power_history, cost[:, i])
+        if is_testing:
+            db.log_test_results(con, setting, i, days, times, *row, impl)
+        else:
+            db.log_validation_results(con, setting, i, days, times, *row, impl)
+    if is_testing:
+        for a in range(len(community.agents)):
+            for r in range(community._rounds + 1):
+                db.log_rounds_decision(con, setting, a, days, times, r, community.decisions[:, r, a].tolist())
+
+
+def load_and_run(is_testing: bool = False, con=None) -> Dict[int, Dict[str, np.ndarray]]:
+    """community.py:364-412: greedy evaluation per test/validation day from the saved tables, a
+    fresh start each day; rows go to the DB when a connection is given (save_community_results);
+    returns per-day power, cost and decisions."""
     setting = setting_name()
     community = get_rl_based_community(setup.nr_agents, homogeneous=setup.homogeneous)
     for agent in community.agents:
@@ -350,5 +380,7 @@ def load_and_run(is_testing: bool = False) -> Dict[int, Dict[str, np.ndarray]]:
             agent_pv = ds.dataframe_to_dataset(agent_dfs[i].loc[day_indices[day], 'pv'] * pr)
             agent.set_profiles(agent_load, agent_pv)
         power, cost = community.run()
+        if con is not None:
+            save_community_results(con, is_testing, setting, int(day), community, np.asarray(cost))
         out[int(day)] = {"power": power, "cost": cost, "decisions": community.decisions.copy()}
     return out

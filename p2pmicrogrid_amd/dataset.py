@@ -15,7 +15,9 @@ synthetic data with the SAME schema and splits:
 """
 from __future__ import annotations
 
+import re
 from dataclasses import dataclass
+from datetime import datetime, timedelta
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -58,9 +60,45 @@ def _day_profiles(rs: np.random.RandomState, days: np.ndarray, shape_prefix=()):
     return dict(time=slot / float(SLOTS_PER_DAY), temperature=temp, pv=pv, loads=np.stack(loads, axis=-2))
 
 
+start_day = min(min(testing_days), min(validation_days), min(training_days))
+end_day = max(max(testing_days), max(validation_days), max(training_days))
+start = datetime(2021, data_month, start_day)
+end = datetime(2021, data_month, end_day) + timedelta(days=1)  # dataset.py:22-25
+
+
+def compute_time_slot(time: str) -> float:
+    """dataset.py:33-36"""
+    t = datetime.strptime(time, '%H:%M:%S')
+    return (t.minute / setup.TIME_SLOT) + t.hour * setup.MINUTES_PER_HOUR / setup.TIME_SLOT
+
+
+def process_dataframe(df: pd.DataFrame) -> pd.DataFrame:
+    """dataset.py:39-54: time slot / 96, loads and PV normalised by their maxima."""
+    df = df.copy()
+    df['time'] = df['time'].map(compute_time_slot) / 96.
+    for c in load_cols:
+        df[c] = df[c].astype(float) / df[c].max().astype(float)
+    df['pv'] = df['pv'].astype(float) / df['pv'].max().astype(float)
+    return df[cols]
+
+
 def get_data(days: List[int], seed: int = 2021) -> Tuple[pd.DataFrame, List[pd.DataFrame]]:
-    """Synthetic stand-in for dataset.get_data (dataset.py:61-80): same columns and
-    normalisation; one frame per load column renamed to 'load' (dataset.py:78)."""
+    """dataset.get_data (dataset.py:61-80).  With a database ($P2PMG_DB, the reference's schema:
+    database.create_tables) the profiles come from it exactly as in the reference; without one
+    (the reference's DB is private) a synthetic generator with the same columns and
+    normalisation stands in.  One frame per load column renamed to 'load' (dataset.py:78)."""
+    from . import database as db
+    con = db.get_connection()
+    if con is not None:
+        try:
+            df = db.get_data(con, start, end)
+        finally:
+            con.close()
+        df['day'] = df['date'].map(lambda d: int(re.match(r'.*-([0-9]+)$', d).groups()[0]))
+        df = df[df['day'].map(lambda d: d in days)]
+        df = process_dataframe(df)
+        agent_dfs = [df[[l] + agent_cols].rename(columns={l: 'load'}) for l in load_cols]
+        return df[env_cols], agent_dfs
     rs = np.random.RandomState(seed + 1000 * min(days))
     prof = _day_profiles(rs, np.asarray(days))
     df = pd.DataFrame({

@@ -165,4 +165,8 @@ class HPHeating(Heating):
         self._t_building_mass = np.array([t_m], np.float32)
 
     def get_history(self) -> List[float]:
+        """heating.py:154-155: T_in before each step of the last run."""
+        return self._history
+
+    def get_history(self) -> List[float]:
         return self._history

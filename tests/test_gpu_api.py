@@ -109,3 +109,27 @@ def test_main_loop_and_npy_checkpoints(tmp_path, monkeypatch):
         assert np.array_equal(saved, a.actor.q_table) and np.count_nonzero(saved) > 0
     out = community.load_and_run(is_testing=True)
     assert len(out) == 5 and all(v["power"].shape == (96, setup.nr_agents) for v in out.values())
+
+
+def test_db_sinks_from_training_and_evaluation(tmp_path, monkeypatch):
+    """main(con) logs training_progress; load_and_run(con) writes test_results rows and the
+    per-round decisions (community.py:333-353) that data_analysis.py reads back."""
+    from p2pmicrogrid_amd import community, database as db, rl, setup
+    monkeypatch.setattr(rl, "MODELS_DIR", str(tmp_path))
+    con = db.get_connection(str(tmp_path / "results.db"))
+    db.create_tables(con.cursor())
+    np.random.seed(42)
+    community.main(episodes=2, verbose=False, con=con)
+    prog = db.get_training_progress(con)
+    assert len(prog) == 2 and prog["episode"].tolist() == [0, 1]
+    out = community.load_and_run(is_testing=True, con=con)
+    res = db.get_test_results(con)
+    N, days = setup.nr_agents, sorted(out)
+    assert len(res) == 96 * N * len(days)
+    for d in days:
+        for i in range(N):
+            rows = res[(res["day"] == d) & (res["agent"] == i)].sort_values("time")
+            assert np.allclose(rows["cost"].values, out[d]["cost"][:, i].astype(np.float64))
+            assert np.allclose(rows["heatpump"].values, out[d]["decisions"][:, -1, i])
+    rd = db.get_rounds_decisions(con)
+    assert len(rd) == 96 * N * len(days) * (setup.rounds + 1)
