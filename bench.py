@@ -63,6 +63,8 @@ def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal only (several ranks on a one-GPU box): every rank on this device
+    local = int(os.environ.get("P2PMG_BENCH_DEVICE", local))
     if world > 1:
         import torch.distributed as dist  # gloo: barrier + max-time only, no GPU interaction
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
