@@ -246,9 +246,65 @@ __device__ __forceinline__ void adam_update(const DqnParams& d, float* th, float
   tg[idx] = d.tau_c * tg[idx] + d.tau * w;
 }
 
+// ReplayBuffer.sample_batch rl.py:226-241 for every agent of the step, ahead of the train kernel:
+// one wave per agent draws 32 distinct deque indices (replayed, or Philox + Floyd as in
+// oracle/philox.py::sample_draws) and gathers the 32 transitions into d.smp [A][32][kTrans], so
+// the train kernel reads one contiguous 1280-B block per agent instead of waiting on 32 random
+// ring reads behind a serial 32-step selection loop.
+__global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
+  const EpisodeParams& p = d.e;
+  const int a = blockIdx.x, l = threadIdx.x;
+  const size_t A = (size_t)p.A;
+  const int n_added = d.added[a];
+  const int count = n_added < d.cap ? n_added : d.cap;
+  const int first = n_added - count;
+  int idx = 0;
+  if (d.samples) {
+    idx = l < kB ? (int)d.samples[((size_t)d.t * A + a) * kB + l] : 0;
+  } else {
+    uint32_t c0 = (uint32_t)d.t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
+             c3 = kTagSample + (uint32_t)(l & 31);
+    philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
+    const int mj = count - kB + (l & 31);
+    const int rj = (int)__umulhi(c0, (uint32_t)(mj + 1));
+    idx = rj;
+    for (int j = 0; j < kB; ++j) {
+      const int r = __shfl(rj, j, 64);
+      const bool taken = __ballot(l < j && idx == r) != 0;
+      if (l == j) idx = taken ? count - kB + j : r;
+    }
+  }
+  if (l < kB) {
+    const float* src = d.buf + ((size_t)a * d.cap + (size_t)((first + idx) % d.cap)) * kTrans;
+    float* dst = d.smp + ((size_t)a * kB + l) * kTrans;
+#pragma unroll
+    for (int k = 0; k < kTrans; ++k) dst[k] = src[k];
+  }
+}
+
+// the weights one train workgroup reads, per lane (wave w owns columns 16w..16w+15)
+// (W2 itself is read per MFMA step from L1/L2: held in registers it costs the second wave per SIMD)
+struct TrainW {
+  float bt0, bo0, bt1, bo1, b1t, b1o, b2t, w3t, b2o, w3o, b3t, b3o;
+};
+__device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const float* tg, int col, int g4) {
+  W.bt0 = tg[kOffW1 + g4 * kH + col];
+  W.bo0 = th[kOffW1 + g4 * kH + col];
+  W.bt1 = g4 == 0 ? tg[kOffW1 + 4 * kH + col] : 0.0f;
+  W.bo1 = g4 == 0 ? th[kOffW1 + 4 * kH + col] : 0.0f;
+  W.b1t = tg[kOffB1 + col];
+  W.b1o = th[kOffB1 + col];
+  W.b2t = tg[kOffB2 + col];
+  W.w3t = tg[kOffW3 + col];
+  W.b2o = th[kOffB2 + col];
+  W.w3o = th[kOffW3 + col];
+  W.b3t = tg[kOffB3];
+  W.b3o = th[kOffB3];
+}
+
 template <bool SHARED>
-__global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
-  __shared__ float smp[kB][kTrans];
+__global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) {  // 2 waves / SIMD
+  __shared__ float smpb[2][kB * kTrans];  // this agent's batch and the next one's (prefetched)
   __shared__ float H1t[3 * kB][kLdsRow];
   __shared__ float H1o[kB][kLdsRow];
   __shared__ float dZ2[kB][kLdsRow];
@@ -265,7 +321,16 @@ __global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
   gW1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   float gb1 = 0.0f, gb2 = 0.0f, gW3 = 0.0f, gb3 = 0.0f;
   const int n_ag = d.batch ? 1 : d.apb;
-  int net = 0;
+  int net = d.batch ? d.net : 0;
+  TrainW W;
+  if (SHARED) load_train_w(W, d.theta + (size_t)net * kNetStride, d.target + (size_t)net * kNetStride, col, g4);
+  // the first agent's batch (explicit batch, or the sample pre-pass output)
+  {
+    const float* src = d.batch ? d.batch : d.smp + (size_t)blockIdx.x * d.apb * (kB * kTrans);
+    const bool ok = d.batch || (size_t)blockIdx.x * d.apb < A;
+    for (int k = threadIdx.x; k < kB * kTrans; k += 256) smpb[0][k] = ok ? src[k] : 0.0f;
+  }
+  __syncthreads();
 
   for (int ag = 0; ag < n_ag; ++ag) {
     const int a = d.batch ? 0 : blockIdx.x * d.apb + ag;
@@ -273,44 +338,19 @@ __global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
     net = d.batch ? d.net : (SHARED ? 0 : a);
     const float* th = d.theta + (size_t)net * kNetStride;
     const float* tg = d.target + (size_t)net * kNetStride;
-
-    // ReplayBuffer.sample_batch rl.py:226-241: 32 distinct transitions
-    if (d.batch) {
-      for (int k = threadIdx.x; k < kB * kTrans; k += 256) smp[k / kTrans][k % kTrans] = d.batch[k];
-    } else {
-      if (w == 0) {
-        const int n_added = d.added[a];
-        const int count = n_added < d.cap ? n_added : d.cap;
-        const int first = n_added - count;
-        int idx = 0;
-        if (d.samples) {
-          idx = l < kB ? (int)d.samples[((size_t)d.t * A + a) * kB + l] : 0;
-        } else {  // Philox + Floyd (oracle/philox.py::sample_draws)
-          uint32_t c0 = (uint32_t)d.t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
-                   c3 = kTagSample + (uint32_t)(l & 31);
-          philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-          const int mj = count - kB + (l & 31);
-          const int rj = (int)__umulhi(c0, (uint32_t)(mj + 1));
-          idx = rj;
-          for (int j = 0; j < kB; ++j) {
-            const int r = __shfl(rj, j, 64);
-            const bool taken = __ballot(l < j && idx == r) != 0;
-            if (l == j) idx = taken ? count - kB + j : r;
-          }
-        }
-        if (l < kB) {
-          const float* src = d.buf + ((size_t)a * d.cap + (size_t)((first + idx) % d.cap)) * kTrans;
-#pragma unroll
-          for (int k = 0; k < kTrans; ++k) smp[l][k] = src[k];
-        }
-      }
+    if (!SHARED) load_train_w(W, th, tg, col, g4);
+    float (*smp)[kTrans] = reinterpret_cast<float (*)[kTrans]>(smpb[ag & 1]);
+    // prefetch the next agent's batch into registers; it goes to the other buffer at the end
+    const bool has_next = !d.batch && ag + 1 < n_ag && a + 1 < (int)A;
+    float nx0 = 0.0f, nx1 = 0.0f;
+    if (has_next) {
+      const float* src = d.smp + (size_t)(a + 1) * (kB * kTrans);
+      nx0 = src[threadIdx.x];
+      if (threadIdx.x < kB * kTrans - 256) nx1 = src[256 + threadIdx.x];
     }
-    __syncthreads();
 
     // ---- layer 1 (K = 5 padded to 8): Z1 = X W1 + b1, 6 target + 2 online row tiles
-    const float bt0 = tg[kOffW1 + g4 * kH + col], bo0 = th[kOffW1 + g4 * kH + col];
-    const float bt1 = g4 == 0 ? tg[kOffW1 + 4 * kH + col] : 0.0f, bo1 = g4 == 0 ? th[kOffW1 + 4 * kH + col] : 0.0f;
-    const float b1t = tg[kOffB1 + col], b1o = th[kOffB1 + col];
+    const float bt0 = W.bt0, bo0 = W.bo0, bt1 = W.bt1, bo1 = W.bo1, b1t = W.b1t, b1o = W.b1o;
     unsigned z1mask = 0;  // online rows where z1 > 0 (ReLU derivative), bit 4 rt + r
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt) {
@@ -342,7 +382,7 @@ __global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt) at[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     ao[0] = ao[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
+#pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const int k = 4 * kk + g4;
       const float bt = tg[kOffW2 + k * kH + col], bo = th[kOffW2 + k * kH + col];
@@ -351,8 +391,7 @@ __global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
       ao[0] = mfma4(H1o[c16][k], bo, ao[0]);
       ao[1] = mfma4(H1o[16 + c16][k], bo, ao[1]);
     }
-    const float b2t = tg[kOffB2 + col], w3t = tg[kOffW3 + col];
-    const float b2o = th[kOffB2 + col], w3o = th[kOffW3 + col];
+    const float b2t = W.b2t, w3t = W.w3t, b2o = W.b2o, w3o = W.w3o;
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt)
 #pragma unroll
@@ -375,7 +414,7 @@ __global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
     __syncthreads();
 
     // ---- targets y = r + gamma * max_a' Q_target(ns, a') and dL/dq (rl.py:314-331)
-    const float b3t = tg[kOffB3], b3o = th[kOffB3];
+    const float b3t = W.b3t, b3o = W.b3o;
     float dq[2][4];
     float lsum = 0.0f, dqsum = 0.0f;
 #pragma unroll
@@ -431,7 +470,7 @@ __global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
       f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
+#pragma unroll
       for (int kk = 0; kk < 16; ++kk) {
         const int j = 4 * kk + g4;
         acc = mfma4(dZ2[16 * rt + c16][j], th[kOffW2 + col * kH + j], acc);
@@ -444,6 +483,10 @@ __global__ __launch_bounds__(256) void dqn_train_kernel(const DqnParams d) {
         const float x = c16 < 5 ? smp[b][c16] : 0.0f;
         gW1 = mfma4(x, dz1, gW1);
       }
+    }
+    if (has_next) {
+      smpb[(ag + 1) & 1][threadIdx.x] = nx0;
+      if (threadIdx.x < kB * kTrans - 256) smpb[(ag + 1) & 1][256 + threadIdx.x] = nx1;
     }
     __syncthreads();  // every wave is done with this agent's LDS and with the online W2
   }
@@ -569,6 +612,11 @@ hipError_t launch_dqn_train(const DqnParams& d, int blocks, bool shared_partials
     hipLaunchKernelGGL(dqn_train_kernel<true>, dim3(blocks), dim3(256), 0, st, d);
   else
     hipLaunchKernelGGL(dqn_train_kernel<false>, dim3(blocks), dim3(256), 0, st, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_dqn_sample(const DqnParams& d, hipStream_t st) {
+  hipLaunchKernelGGL(dqn_sample_kernel, dim3(d.e.A), dim3(kWave), 0, st, d);
   return hipGetLastError();
 }
 

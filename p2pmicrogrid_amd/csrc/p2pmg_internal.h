@@ -85,6 +85,7 @@ struct DqnParams {
   int32_t* added;            // [A] transitions ever added
   int cap;
   const uint16_t* samples;   // replay mode: [T][A][32] deque indices; null = Philox (Floyd)
+  float* smp;                // [A][32][kTrans] this step's sampled transitions (dqn_sample_kernel)
   float* rec_loss;           // [T][A] or null
   float* ep_acc;             // [S] running sum_t mean_i r
   float gamma, tau, tau_c, lr_t, b1c, b2c, adam_eps, clip;
@@ -95,6 +96,7 @@ struct DqnParams {
   float* loss_out;           // explicit batch: [1]
 };
 hipError_t launch_dqn_act(const DqnParams& p, hipStream_t stream);
+hipError_t launch_dqn_sample(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_train(const DqnParams& p, int blocks, bool shared_partials, hipStream_t stream);
 hipError_t launch_dqn_reduce(const DqnParams& p, int n_partials, hipStream_t stream);
 hipError_t launch_dqn_adam_shared(const DqnParams& p, hipStream_t stream);

@@ -87,6 +87,7 @@ struct p2pmg_ctx {
   float* d_v = nullptr;
   float* d_grad = nullptr;    // shared network: [d_blocks][kNetStride] partials
   float* d_gsum = nullptr;    // [kNetStride]
+  float* d_smp = nullptr;     // [A][32][kTrans] sampled batches of the current step
   int d_blocks = 0, d_apb = 1;
   float* d_buf = nullptr;     // [A][capacity][10]
   int32_t* d_added = nullptr; // [A]
@@ -337,6 +338,7 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   dfree(c->d_v);
   dfree(c->d_grad);
   dfree(c->d_gsum);
+  dfree(c->d_smp);
   dfree(c->d_buf);
   dfree(c->d_added);
   dfree(c->d_samples);
@@ -1143,6 +1145,7 @@ int p2pmg_dqn_setup(p2pmg_ctx* c, const p2pmg_dqn_config* cfg) {
   }
   HIP_TRY(c, dmalloc(&c->d_buf, A * (size_t)cfg->capacity * p2pmg::kTrans));
   HIP_TRY(c, dmalloc(&c->d_added, A));
+  HIP_TRY(c, dmalloc(&c->d_smp, A * p2pmg::kDqnBatch * p2pmg::kTrans));
   HIP_TRY(c, hipMemsetAsync(c->d_added, 0, A * 4, c->stream));
   HIP_TRY(c, dmalloc(&c->d_ep_acc, (size_t)c->S));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1267,6 +1270,7 @@ static p2pmg::DqnParams dqn_params(p2pmg_ctx* c, const EpisodeParams& e) {
   d.adam_m = c->d_m;
   d.adam_v = c->d_v;
   d.grad = c->d_grad;
+  d.smp = c->d_smp;
   d.gsum = c->d_gsum;
   d.buf = c->d_buf;
   d.added = c->d_added;
@@ -1295,6 +1299,7 @@ static float adam_lr(const p2pmg_dqn_config& q, int64_t step) {
 static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d) {
   c->d_step++;
   d.lr_t = adam_lr(c->dcfg, c->d_step);
+  HIP_TRY(c, p2pmg::launch_dqn_sample(d, c->stream));
   if (c->n_nets == 1) {
     HIP_TRY(c, p2pmg::launch_dqn_train(d, c->d_blocks, true, c->stream));
     HIP_TRY(c, p2pmg::launch_dqn_reduce(d, c->d_blocks, c->stream));
