@@ -9,11 +9,13 @@ The reference draws exploration from the global legacy ``np.random`` MT19937 str
 SURVEY.md §3.5 (ii): one Philox block per (seed, episode, agent, t, round, tag), so the
 result is independent of how scenarios are sharded over GPUs.
 
-Block layout (must match ``p2pmicrogrid_amd/csrc/p2pmg.hip::philox_decision``):
+Block layout (must match ``p2pmicrogrid_amd/csrc/p2pmg_kernels.hip::philox_code_pair``): one
+block serves two negotiation rounds, P = ceil((R + 1) / 2) blocks per agent-step:
     key  = (seed_lo, seed_hi)
-    ctr  = (t * (R + 1) + r, episode, agent_global, TAG)
-    u    = ((x0 >> 5) * 2**26 + (x1 >> 6)) / 2**53          (NumPy's rand() formula)
-    act  = (x2 * 3) >> 32                                     (multiply-high, 3 actions)
+    ctr  = (t * P + r // 2, episode, agent_global, TAG_DECISION)
+    q    = r % 2
+    u    = x[2q] / 2**32                                      (exact in f64)
+    act  = (x[2q+1] * 3) >> 32                                (multiply-high, 3 actions)
     explore <=> u < epsilon   (f64 compare, as rl.py:101)
 T0 draws at an episode start (tag TAG_T0, ctr = (0, episode, agent, TAG_T0)):
     Box-Muller in f64 on u1 = (x0 + 0.5) / 2**32, u2 = (x1 + 0.5) / 2**32;
@@ -29,7 +31,7 @@ W0 = np.uint64(0x9E3779B9)
 W1 = np.uint64(0xBB67AE85)
 MASK32 = np.uint64(0xFFFFFFFF)
 
-TAG_DECISION = 0x5EED0001
+TAG_DECISION = 0x5EED0003  # two rounds per block (0x5EED0001 was one block per round)
 TAG_T0 = 0x5EED0002
 
 
@@ -56,15 +58,15 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
 
 
 def decision_draws(seed: int, episode: int, agents, t: int, r: int, rounds: int):
-    """(u f64, action int) for each agent id in ``agents`` at (episode, t, r)."""
+    """(u f64, action int) for each agent id in ``agents`` at (episode, t, r); ``rounds`` = R."""
     agents = np.asarray(agents, dtype=np.uint64)
     k0 = seed & 0xFFFFFFFF
     k1 = (seed >> 32) & 0xFFFFFFFF
-    x0, x1, x2, _ = philox4x32_10(t * (rounds + 1) + r, episode, agents, TAG_DECISION, k0, k1)
-    a = (x0 >> np.uint64(5)).astype(np.float64)
-    b = (x1 >> np.uint64(6)).astype(np.float64)
-    u = (a * 67108864.0 + b) / 9007199254740992.0
-    act = ((x2 * np.uint64(3)) >> np.uint64(32)).astype(np.int64)
+    pairs = (rounds + 2) // 2
+    x = philox4x32_10(t * pairs + r // 2, episode, agents, TAG_DECISION, k0, k1)
+    q = r % 2
+    u = x[2 * q].astype(np.float64) / 4294967296.0
+    act = ((x[2 * q + 1] * np.uint64(3)) >> np.uint64(32)).astype(np.int64)
     return u, act
 
 

@@ -55,7 +55,7 @@ __device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32
     c3 = lo0;
   }
 }
-constexpr uint32_t kTagDecision = 0x5EED0001u;
+constexpr uint32_t kTagDecision = 0x5EED0003u;  // one block per two rounds (oracle/philox.py)
 constexpr uint32_t kTagT0 = 0x5EED0002u;
 
 // RuleAgent._update_storage (agent.py:138-153) with BatteryStorage bookkeeping (storage.py:79-100),

@@ -107,11 +107,12 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
       if (p.rng == 0) {
         code = (int)((p.codes[((size_t)t * W + (r >> 2)) * A + a] >> (8 * (r & 3))) & 0xFFu);
       } else {
-        uint32_t c0 = (uint32_t)(t * R1 + r), c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
-                 c3 = kTagDecision;
+        // one Philox block per two rounds (oracle/philox.py::decision_draws)
+        uint32_t c0 = (uint32_t)(t * ((R1 + 1) >> 1) + (r >> 1)), c1 = (uint32_t)p.episode,
+                 c2 = p.agent_offset + (uint32_t)a, c3 = kTagDecision;
         philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-        const double u = ((double)(c0 >> 5) * 67108864.0 + (double)(c1 >> 6)) * (1.0 / 9007199254740992.0);
-        code = u < p.eps ? (int)__umulhi(c2, 3u) : 255;
+        const uint32_t wu = (r & 1) ? c2 : c0, wa = (r & 1) ? c3 : c1;
+        code = (double)wu * (1.0 / 4294967296.0) < p.eps ? (int)__umulhi(wa, 3u) : 255;
       }
     }
     if (code == 255) {

@@ -281,12 +281,20 @@ __device__ __forceinline__ StepIdx make_step(const KC& p, const Dims<B20>& D, bo
   return st;
 }
 
-// Philox exploration draw for (t, r): 255 = greedy (QActor.select_action rl.py:100-111)
-__device__ __forceinline__ uint32_t philox_code(const EpisodeParams& p, int t, int r, uint32_t gid) {
-  uint32_t c0 = (uint32_t)(t * (p.R + 1) + r), c1 = (uint32_t)p.episode, c2 = gid, c3 = kTagDecision;
+// Philox exploration draws of rounds 2 pair and 2 pair + 1 at step t from ONE block: code of
+// round 2 pair in bits 0..7, of round 2 pair + 1 in bits 8..15; 255 = greedy
+// (QActor.select_action rl.py:100-111).  Layout: oracle/philox.py::decision_draws.
+__device__ __forceinline__ uint32_t philox_code_pair(const EpisodeParams& p, int t, int pair, uint32_t gid) {
+  const int pairs = (p.R + 2) >> 1;
+  uint32_t c0 = (uint32_t)(t * pairs + pair), c1 = (uint32_t)p.episode, c2 = gid, c3 = kTagDecision;
   philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-  const double u = ((double)(c0 >> 5) * 67108864.0 + (double)(c1 >> 6)) / 9007199254740992.0;
-  return u < p.eps ? (uint32_t)(((uint64_t)c2 * 3ull) >> 32) : 255u;
+  const uint32_t a0 = (uint32_t)(((uint64_t)c1 * 3ull) >> 32), a1 = (uint32_t)(((uint64_t)c3 * 3ull) >> 32);
+  const uint32_t k0 = (double)c0 * (1.0 / 4294967296.0) < p.eps ? a0 : 255u;
+  const uint32_t k1 = (double)c2 * (1.0 / 4294967296.0) < p.eps ? a1 : 255u;
+  return k0 | (k1 << 8);
+}
+__device__ __forceinline__ uint32_t philox_code(const EpisodeParams& p, int t, int r, uint32_t gid) {
+  return (philox_code_pair(p, t, r >> 1, gid) >> (8 * (r & 1))) & 0xFFu;
 }
 
 // all rounds' codes of step t packed one byte per round (round r in bits 8r..8r+7)
@@ -305,9 +313,9 @@ __device__ __forceinline__ CodeWords step_codes(const EpisodeParams& p, const ui
   c.w1 = codes_a[W > 1 ? off + (size_t)p.A : off];
   c.gen = ~0ull;
   if (p.rng == 1) {
-    for (int r = 0; r <= p.R; ++r) {
-      const uint64_t v = philox_code(p, t, r, p.agent_offset + (uint32_t)a);
-      c.gen = (c.gen & ~(0xFFull << (8 * r))) | (v << (8 * r));
+    for (int r = 0; r <= p.R; r += 2) {
+      const uint64_t v = philox_code_pair(p, t, r >> 1, p.agent_offset + (uint32_t)a);
+      c.gen = (c.gen & ~(0xFFFFull << (8 * r))) | (v << (8 * r));
     }
   }
   return c;
@@ -730,9 +738,10 @@ __global__ void philox_codes_kernel(const EpisodeParams p, uint32_t* __restrict_
   const int R1 = p.R + 1, W = (R1 + 3) >> 2;
   for (int w = 0; w < W; ++w) {
     uint32_t word = 0xFFFFFFFFu;
-    for (int b = 0; b < 4 && 4 * w + b < R1; ++b) {
-      const uint32_t c = philox_code(p, t, 4 * w + b, p.agent_offset + (uint32_t)a);
-      word = (word & ~(0xFFu << (8 * b))) | (c << (8 * b));
+    for (int b = 0; b < 4 && 4 * w + b < R1; b += 2) {
+      uint32_t c = philox_code_pair(p, t, (4 * w + b) >> 1, p.agent_offset + (uint32_t)a);
+      if (4 * w + b + 1 >= R1) c |= 0xFF00u;
+      word = (word & ~(0xFFFFu << (8 * b))) | (c << (8 * b));
     }
     words[((size_t)t * W + w) * p.A + a] = word;
   }
@@ -872,9 +881,10 @@ __device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOu
     const int R1 = p.R + 1, W = (R1 + 3) >> 2;
     for (int w = 0; w < W; ++w) {
       uint32_t word = 0xFFFFFFFFu;
-      for (int b = 0; b < 4 && 4 * w + b < R1; ++b) {
-        const uint32_t c = philox_code(q, t, 4 * w + b, p.agent_offset + (uint32_t)a);
-        word = (word & ~(0xFFu << (8 * b))) | (c << (8 * b));
+      for (int b = 0; b < 4 && 4 * w + b < R1; b += 2) {
+        uint32_t c = philox_code_pair(q, t, (4 * w + b) >> 1, p.agent_offset + (uint32_t)a);
+        if (4 * w + b + 1 >= R1) c |= 0xFF00u;
+        word = (word & ~(0xFFFFu << (8 * b))) | (c << (8 * b));
       }
       o.words[((size_t)t * W + w) * p.A + a] = word;
     }
