@@ -1311,6 +1311,24 @@ hipError_t launch_fast_q(const EpisodeParams& p, const uint2* pre, void* recs, i
 
 // ----------------------------------------------------------------- the fast shared-table path (N = 16)
 typedef float pkf2 __attribute__((ext_vector_type(2)));
+// v with lane (16 k + J) set to +0 for every k: the diagonal of a 16-agent scenario whose agent i
+// sits in lane i of its 16-lane group.  The lane pattern is a constant loaded into VCC right at the
+// use: as a C++ compare, the 16 loop-invariant masks get hoisted into 32 SGPRs, spill to VGPR lanes
+// and cost two v_readlane per use.
+template <int J>
+__device__ __forceinline__ float zero_diag16(float v) {
+  float r;
+  asm volatile("s_mov_b32 vcc_lo, %2\n\ts_mov_b32 vcc_hi, %2\n\tv_cndmask_b32_e64 %0, %1, 0, vcc"
+               : "=v"(r) : "v"(v), "i"(0x00010001u << J) : "vcc");
+  return r;
+}
+template <int J = 0>
+__device__ __forceinline__ void zero_diag16_all(float (&col)[16]) {
+  if constexpr (J < 16) {
+    col[J] = zero_diag16<J>(col[J]);
+    zero_diag16_all<J + 1>(col);
+  }
+}
 // 0 or |x| in [2^-19, 2^19]: products of two such numbers are 0 or in [2^-38, 2^38]
 __device__ __forceinline__ bool in_range19(float x) {
   const float m = fabsf(x);
@@ -1545,9 +1563,10 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
         col[4 * m] = v.x; col[4 * m + 1] = v.y; col[4 * m + 2] = v.z; col[4 * m + 3] = v.w;
       }
       wave_lds_fence();
+      zero_diag16_all(col);  // powers = -P[:, i] with P's diagonal zeroed (community.py:76,81)
       float acc = 0.0f;
 #pragma unroll
-      for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : col[j]));
+      for (int j = 0; j < N; ++j) acc = acc + (-col[j]);
       ip = idx_plain(fdiv_b(div_n<N>(acc), rmi), D.p());
       code = (int)((cw >> 8) & 0xFF);
       const bool need = code == 255 || TRAIN;
@@ -1566,7 +1585,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
       float tot = 0.0f;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
-        f[j] = __builtin_amdgcn_fmed3f(-((j == i) ? 0.0f : col[j]), flo, fhi);
+        f[j] = __builtin_amdgcn_fmed3f(-col[j], flo, fhi);
         tot = tot + f[j];
       }
       tot = fabsf(tot);
