@@ -1479,17 +1479,20 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, D.p());
   const int R1r = p.R + 1, W = (R1r + 3) >> 2;
 
+  // running element offsets in 32 bits (the launcher checks T * A * W < 2^32 and the env table
+  // size): fewer 64-bit uniform values live across the loop, i.e. fewer SGPR spills
   const float* envb = p.env + (size_t)s_env * kEnvStride;
-  const size_t env_step = (size_t)p.n_env * kEnvStride;
-  const size_t env_end = env_step * T;
+  const uint32_t env_step = (uint32_t)p.n_env * kEnvStride;
+  const uint32_t env_end = env_step * (uint32_t)T;
   const float2* profb = p.prof + a;
-  const size_t prof_end = A * T;
+  const uint32_t A32 = (uint32_t)p.A;
+  const uint32_t prof_end = A32 * (uint32_t)T;
   const uint32_t* codes_a = p.codes + a;
-  const size_t code_step = (size_t)W * A;
-  auto adv = [](size_t off, size_t step, size_t end) { off += step; return off >= end ? off - end : off; };
-  size_t e1o = adv(0, env_step, env_end), e2o = adv(e1o, env_step, env_end);
-  size_t f1o = adv(0, A, prof_end), f2o = adv(f1o, A, prof_end);
-  size_t c1o = (T > 1) ? code_step : 0;
+  const uint32_t code_step = (uint32_t)W * A32;
+  auto adv = [](uint32_t off, uint32_t step, uint32_t end) { off += step; return off >= end ? off - end : off; };
+  uint32_t e1o = adv(0, env_step, env_end), e2o = adv(e1o, env_step, env_end);
+  uint32_t f1o = adv(0, A32, prof_end), f2o = adv(f1o, A32, prof_end);
+  uint32_t c1o = (T > 1) ? code_step : 0;
   // records: FastRec rows, or only {reward, cost} as float2 when nothing else was requested
   // (8 B instead of 32 B of writes per agent-step); masked-off lanes write a dummy row
   const bool narrow = p.rec_narrow != 0;
@@ -1708,8 +1711,8 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     e1 = e2;
     f1 = f2;
     e2o = adv(e2o, env_step, env_end);
-    f2o = adv(f2o, A, prof_end);
-    c1o = (t + 2 >= T) ? (size_t)0 : c1o + code_step;
+    f2o = adv(f2o, A32, prof_end);
+    c1o = (t + 2 >= T) ? 0u : c1o + code_step;
     st = st1;
     cw = cw1;
     a0 = a0n;

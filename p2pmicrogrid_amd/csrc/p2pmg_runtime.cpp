@@ -635,6 +635,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
                     !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_PHILOX_INKERNEL)) && !env_general;
   // shared table, 16-agent scenarios (configs[2]): episode_sq16_kernel
   const bool sq16 = g.shared_q && c->N == 16 && c->R <= 1 && c->mi_ok && host_div_range(g.minutes_per_hour) &&
+                    (long long)c->T * c->A < (1LL << 32) && (long long)c->T * c->n_env * p2pmg::kEnvStride < (1LL << 32) &&
                     host_div_range(g.temp_margin) && g.n_time_states == 20 && g.n_temp_states == 20 &&
                     g.n_balance_states == 20 && g.n_p2p_states == 20 &&
                     !(args->flags & P2PMG_FLAG_GENERAL_KERNEL) && !env_general;
