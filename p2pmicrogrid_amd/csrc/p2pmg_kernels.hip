@@ -1639,24 +1639,20 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
 #pragma unroll
     for (int j = 0; j < N; ++j) col[j] = tp[j * 16 + cofs[j & 3]];
     wave_lds_fence();
-    // (g, pp) as one packed pair: g += pij - ex and pp += ex in one v_pk_add_f32 per j, the
-    // differences two j at a time (each lane of a packed op rounds like the scalar op)
-    pkf2 gp = {0.0f, 0.0f};
+    // ex = sign(pij) min(|pij|, |pji|) where the sign bits differ, else +0: one v_min with abs
+    // modifiers (as C++ the compiler canonicalises both operands first), v_bfi for the sign, and
+    // the sign test as an arithmetic-shift mask
+    float g = 0.0f, pp = 0.0f;
 #pragma unroll
-    for (int j = 0; j < N; j += 2) {
-      float ex[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const float pij = row[j + u], pji = col[j + u];
-        const float mn = __builtin_amdgcn_fmed3f(fabsf(pij), fabsf(pji), -__builtin_inff());
-        const bool opp = ((__float_as_uint(pij) ^ __float_as_uint(pji)) >> 31) != 0u;
-        ex[u] = opp ? __builtin_copysignf(mn, pij) : 0.0f;
-      }
-      const pkf2 d = pkf2{row[j], row[j + 1]} - pkf2{ex[0], ex[1]};
-      gp = gp + pkf2{d.x, ex[0]};
-      gp = gp + pkf2{d.y, ex[1]};
+    for (int j = 0; j < N; ++j) {
+      const float pij = row[j], pji = col[j];
+      float mn;
+      asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(mn) : "v"(pij), "v"(pji));
+      const int opp = (__float_as_int(pij) ^ __float_as_int(pji)) >> 31;
+      const float ex = __int_as_float(__float_as_int(__builtin_copysignf(mn, pij)) & opp);
+      g = g + (pij - ex);
+      pp = pp + ex;
     }
-    const float g = gp.x, pp = gp.y;
     float cost = (g >= 0.0f) ? g * e0.buy : g * e0.inj;
     cost = cost + pp * e0.p2p;
     cost = fdiv_b(cost * k.slot, rmph);
