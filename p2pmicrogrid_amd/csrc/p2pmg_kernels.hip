@@ -357,6 +357,14 @@ __device__ __forceinline__ Row4<QT> patched(Row4<QT> r, uint32_t addr, const Pat
 // a global load + vmcnt(0) on the critical path)
 __device__ __forceinline__ float hp_of(const float4& lv, int act) { return sel3(act, lv.x, lv.y, lv.z); }
 
+// min(|a|, |b|) as one v_min_f32 with abs modifiers (written as C++, hipcc first canonicalises each
+// operand with a v_max; operands here are never NaN, so the plain v_min is the same value)
+__device__ __forceinline__ float min_abs(float a, float b) {
+  float r;
+  asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // ----------------------------------------------------------------- the episode kernel
 // One launch = one episode of T timesteps for every scenario (train_episode / run).
 // Latency structure per step (one dependent Q gather per extra round):
@@ -1163,7 +1171,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       // zero operand min(...) = 0, so ex = +-0 and g, pp (which start at +0) take the same values
       // as with the reference's 0; otherwise "signs differ" is "sign bits differ".
       const float pij = row[j], pji = col[j];
-      const float mn = __builtin_amdgcn_fmed3f(fabsf(pij), fabsf(pji), -__builtin_inff());  // min of the two
+      const float mn = min_abs(pij, pji);
       const bool opp = ((__float_as_uint(pij) ^ __float_as_uint(pji)) >> 31) != 0u;
       const float ex = opp ? __builtin_copysignf(mn, pij) : 0.0f;
       g = g + (pij - ex);
@@ -1646,8 +1654,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const float pij = row[j], pji = col[j];
-      float mn;
-      asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(mn) : "v"(pij), "v"(pji));
+      const float mn = min_abs(pij, pji);
       const int opp = (__float_as_int(pij) ^ __float_as_int(pji)) >> 31;
       const float ex = __int_as_float(__float_as_int(__builtin_copysignf(mn, pij)) & opp);
       g = g + (pij - ex);
@@ -1787,7 +1794,7 @@ __global__ __launch_bounds__(kWave) void rule_episode_kernel(const EpisodeParams
     float g = 0.0f, pp = 0.0f;
     for (int j = 0; j < N; ++j) {
       const float pj = shP[sl * G + j];
-      const float mn = fminf(fabsf(P), fabsf(pj));
+      const float mn = min_abs(P, pj);
       const bool opp = ((__float_as_uint(P) ^ __float_as_uint(pj)) >> 31) != 0u;
       const float ex = opp ? __builtin_copysignf(mn, P) : 0.0f;
       g = g + (P - ex);
