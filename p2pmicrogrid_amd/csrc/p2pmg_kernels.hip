@@ -32,27 +32,38 @@ struct Row4 {
 
 // x[a] for a in {0,1,2} as two v_cndmask: written in asm because hipcc turns a select chain
 // on a runtime index into a scratch/LDS lookup table (a memory round trip + vmcnt(0) drain)
-__device__ __forceinline__ float sel3(int a, float x0, float x1, float x2) {
+// 3-way select by a per-lane index a in {0, 1, 2}, as asm so that hipcc never turns it into a
+// scratch-indexed array.  The two lane masks are separate (non-volatile) asm: every select on the
+// same index shares them (CSE), e.g. the six 32-bit halves of a selected f64 row.
+struct Sel3M {
+  uint64_t m1, m2;
+};
+__device__ __forceinline__ Sel3M sel3_masks(int a) {
+  uint64_t m1, m2;
+  asm("v_cmp_eq_u32_e64 %0, 1, %1" : "=s"(m1) : "v"(a));
+  asm("v_cmp_eq_u32_e64 %0, 2, %1" : "=s"(m2) : "v"(a));
+  return Sel3M{m1, m2};
+}
+__device__ __forceinline__ float sel3(const Sel3M& m, float x0, float x1, float x2) {
   float r;
-  asm volatile(
-      "v_cmp_eq_u32 vcc, 1, %1\n\t"
-      "v_cndmask_b32 %0, %2, %3, vcc\n\t"
-      "v_cmp_eq_u32 vcc, 2, %1\n\t"
-      "v_cndmask_b32 %0, %0, %4, vcc"
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3\n\tv_cndmask_b32_e64 %0, %0, %4, %5"
       : "=&v"(r)
-      : "v"(a), "v"(x0), "v"(x1), "v"(x2)
-      : "vcc");
+      : "v"(x0), "v"(x1), "s"(m.m1), "v"(x2), "s"(m.m2));
   return r;
 }
-__device__ __forceinline__ double sel3(int a, double x0, double x1, double x2) {
+__device__ __forceinline__ double sel3(const Sel3M& m, double x0, double x1, double x2) {
   const uint64_t b0 = (uint64_t)__double_as_longlong(x0), b1 = (uint64_t)__double_as_longlong(x1),
                  b2 = (uint64_t)__double_as_longlong(x2);
-  const uint32_t lo = __float_as_uint(sel3(a, __uint_as_float((uint32_t)b0), __uint_as_float((uint32_t)b1),
+  const uint32_t lo = __float_as_uint(sel3(m, __uint_as_float((uint32_t)b0), __uint_as_float((uint32_t)b1),
                                            __uint_as_float((uint32_t)b2)));
-  const uint32_t hi = __float_as_uint(sel3(a, __uint_as_float((uint32_t)(b0 >> 32)),
+  const uint32_t hi = __float_as_uint(sel3(m, __uint_as_float((uint32_t)(b0 >> 32)),
                                            __uint_as_float((uint32_t)(b1 >> 32)),
                                            __uint_as_float((uint32_t)(b2 >> 32))));
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <typename T>
+__device__ __forceinline__ T sel3(int a, T x0, T x1, T x2) {
+  return sel3(sel3_masks(a), x0, x1, x2);
 }
 // Timing-only ablation builds (scripts/latency_ablation.py): -DP2PMG_ABLATE=1 replaces the
 // episode kernel's Q-row gathers by values derived from the address (no memory access),
@@ -339,8 +350,9 @@ struct Patch {
 template <typename QT>
 __device__ __forceinline__ Row4<QT> sel_row(int b, const Row4<QT>& x0, const Row4<QT>& x1, const Row4<QT>& x2) {
   Row4<QT> r;
+  const Sel3M m = sel3_masks(b);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) r.v[k] = sel3(b, x0.v[k], x1.v[k], x2.v[k]);
+  for (int k = 0; k < 3; ++k) r.v[k] = sel3(m, x0.v[k], x1.v[k], x2.v[k]);
   r.v[3] = (QT)0;
   return r;
 }
