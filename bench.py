@@ -13,6 +13,11 @@ N GPUs: one process per GPU (torchrun), scenarios sharded with no data-path coll
 scenario's tables are private: "replicas only"); torch.distributed(gloo) carries only the
 barrier and the max-over-ranks time.  value = all ranks' agent-steps / max time (weak scaling).
 
+``--workload config4`` (BASELINE.json configs[3]): 4096 scenarios x 4 households per GPU with
+heterogeneous asset mixes (dataset.asset_mix: Consumers without PV, no / 3 kW / 5 kW heat pumps,
+10 kWh battery or NoStorage), one-year episodes (T = 35,040 quarter-hour slots), per-agent f64
+Q-tables (84 GB per GPU): replicas only, like configs[1].
+
 ``--workload config3`` (BASELINE.json configs[2]): 1M scenarios x 16 agents with battery storage
 over 8 GPUs = 125,000 scenarios (2M agents) per GPU, ONE shared f32 Q-table whose int64
 fixed-point TD deltas are all-reduced over RCCL once per episode (the path's real exchange step).
@@ -95,7 +100,10 @@ WORKLOADS = {
     "config2": (4096, 2, 1, 96, "f64", False, False),
     "config3": (125000, 16, 1, 96, "f32", True, True),
     "config5": (4096, 2, 1, 96, "f32", True, False),  # DQN, one shared network (data-parallel)
+    # configs[3]: heterogeneous PV / heat-pump / battery mixes, 1-year episodes, per-agent tables
+    "config4": (4096, 4, 1, 365 * 96, "f64", False, True),
 }
+HETERO = {"config4"}
 
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_16x16x4_f32) = f32 vector rate
 DQN_FWD_FLOP = 2 * (5 * 64 + 64 * 64 + 64 * 1)  # QNetwork (rl.py:135-148): 8,960 FLOP per row
@@ -204,15 +212,25 @@ def main_dqn(args, rank, world, local, S, N, R, T):
 
 
 def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 96, q_dtype: str = "f64",
-                 shared: bool = False, battery: bool = False):
+                 shared: bool = False, battery: bool = False, hetero: bool = False, t_sample: int = 0):
     """The oracle (NumPy CPU restatement, oracle/restatement.py) on a bounded sample of the same
-    workload, single-threaded, Philox exploration."""
+    workload, single-threaded, Philox exploration.  t_sample > 0: episodes cut to the first
+    t_sample slots of the generated horizon (per-step cost does not depend on T)."""
     from oracle.restatement import OracleBatch
-    from p2pmicrogrid_amd.dataset import scenario_batch
+    from p2pmicrogrid_amd.dataset import apply_asset_mix, asset_mix, scenario_batch
     inp = scenario_batch(S, N, T)
+    lv, cap = None, (np.full((S, N), BATTERY_J) if battery else None)
+    if hetero:
+        mix = asset_mix(S, N, battery_j=BATTERY_J)
+        inp, lv, cap = apply_asset_mix(inp, mix), mix.hp_levels, mix.battery_capacity
+    full_T = T
+    if t_sample and t_sample < T:
+        T = t_sample
+        inp.load_w, inp.pv_w, inp.t_out = inp.load_w[..., :T], inp.pv_w[..., :T], inp.t_out[..., :T]
+        inp.time = inp.time[:T]
     ob = OracleBatch(S=S, N=N, R=R, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in,
                      env_time=inp.time[None], env_tout=inp.t_out, q_dtype=q_dtype, shared_q=shared,
-                     battery_capacity=np.full((S, N), BATTERY_J) if battery else None)
+                     hp_levels=lv, battery_capacity=cap)
     ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
     t0 = time.perf_counter()
     eps_done = 0
@@ -225,6 +243,8 @@ def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 
             break
     dt = time.perf_counter() - t0
     what = "shared table + battery, " if shared else ""
+    if hetero:
+        what = f"heterogeneous mixes + battery, first {T} of {full_T} slots, "
     return {"value": S * N * T * eps_done / dt, "unit": "agent-steps/s", "cores": 1, "kind": "port",
             "sample": f"{S} scenarios x N={N} (R={R}, T={T}, {what}{q_dtype} Q), {eps_done} training episodes, "
                       f"oracle/restatement.py vectorised NumPy, {dt:.1f} s"}
@@ -249,7 +269,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50, help="timed episodes")
     ap.add_argument("--warmup", type=int, default=5, help="untimed episodes")
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS),
-                    help="config2 = BASELINE configs[1] (default); config3 = configs[2] per-GPU slice")
+                    help="config2 = BASELINE configs[1] (default); config3 = configs[2] per-GPU slice; "
+                         "config4 = configs[3]; config5 = configs[4] (DQN)")
     ap.add_argument("--scenarios", type=int, default=None, help="override scenarios per GPU")
     ap.add_argument("--agents", type=int, default=None)
     ap.add_argument("--rounds", type=int, default=None)
@@ -262,10 +283,11 @@ def main():
     args = ap.parse_args()
 
     rank, world, local = dist_setup()
-    from p2pmicrogrid_amd.dataset import scenario_batch
+    from p2pmicrogrid_amd.dataset import apply_asset_mix, asset_mix, scenario_batch
     from p2pmicrogrid_amd.engine import DeviceCommunityBatch
 
     S, N, R, T, q_dtype, shared, battery = WORKLOADS[args.workload]
+    hetero = args.workload in HETERO
     S = args.scenarios or S
     N = args.agents or N
     R = R if args.rounds is None else args.rounds
@@ -275,13 +297,20 @@ def main():
         return main_dqn(args, rank, world, local, S, N, R, T)
     first = rank * S
     inp = scenario_batch(S, N, T, first_scenario=first)
+    mix = None
+    if hetero:
+        mix = asset_mix(S, N, first_scenario=first, battery_j=BATTERY_J)
+        inp = apply_asset_mix(inp, mix)
     eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=local, scenario_offset=first, shared_q=shared)
     eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
     eng.set_profiles(inp.load_w, inp.pv_w)
     eng.set_max_in(inp.max_in)
     eng.set_temperatures(inp.t_in0, inp.t_m0)
     del inp
-    if battery:
+    if mix is not None:
+        eng.set_hp_levels(mix.hp_levels)
+        eng.set_battery(mix.battery_capacity)
+    elif battery:
         eng.set_battery(BATTERY_J)
     if shared and world > 1:  # RCCL communicator for the per-episode delta all-reduce (xGMI)
         from p2pmicrogrid_amd.distributed import broadcast_bytes
@@ -322,6 +351,11 @@ def main():
         bpa = algorithmic_bytes_per_agent_step_shared(S * N, q_bytes, battery, outputs=len(record))
         workload = (f"configs[2]: {S} scenarios/GPU x {N} agents (R={R}, T={T}) with battery storage, one shared "
                     f"{q_dtype} Q-table, int64 delta all-reduce per episode, Philox exploration, train episodes")
+    elif hetero:
+        bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
+        workload = (f"configs[3]: {S} scenarios/GPU x {N} heterogeneous households (R={R}, T={T} = "
+                    f"{T // 96} days; no-PV / heat-pump size / battery mixes), per-agent {q_dtype} Q-tables, "
+                    f"Philox exploration, train episodes")
     else:
         bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
         workload = (f"configs[1]: {S} scenarios/GPU x thesis community (N={N}, R={R}, T={T}), per-agent "
@@ -363,8 +397,9 @@ def main():
         if traffic:
             out["roofline"]["traffic_source"] = traffic.get("source")
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, S=256 if N <= 4 else 64, N=N, R=R, T=T,
-                                               q_dtype=q_dtype, shared=shared, battery=battery)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, S=(64 if hetero else 256) if N <= 4 else 64,
+                                               N=N, R=R, T=T, q_dtype=q_dtype, shared=shared, battery=battery,
+                                               hetero=hetero, t_sample=960 if T > 960 else 0)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

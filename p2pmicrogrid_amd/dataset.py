@@ -213,3 +213,54 @@ def scenario_batch(S: int, N: int, T: int = SLOTS_PER_DAY, seed: int = setup.see
     return ScenarioInputs(time=time, t_out=t_out, load_w=sl['load_w'], pv_w=sl['pv_w'], max_in=sl['max_in'],
                           t_in0=sl['t_in0'], t_m0=sl['t_m0'], load_ratings=sl['load_ratings'],
                           pv_ratings=sl['pv_ratings'])
+
+
+# ----------------------------------------------------------------------------- heterogeneous mixes
+@dataclass
+class AssetMix:
+    """Per-agent asset mix of a heterogeneous community (BASELINE.json configs[3]).
+
+    The reference builds every household as PV + 3 kW heat pump + NoStorage (community.py:219-228);
+    the mixes are the build's extension along the reference's own asset classes: ``Consumer`` (no PV,
+    production.py:44-58), a heat pump of another size (``HeatPump(cop, max_power, power)``,
+    heating.py:158-163) or none, and ``BatteryStorage`` (storage.py:36-76) or ``NoStorage``."""
+    has_pv: np.ndarray            # [S, N] bool
+    hp_levels: np.ndarray         # [S, N, 3] f32 heat-pump power per action (0 = no heat pump)
+    battery_capacity: np.ndarray  # [S, N] f64 J (0 = NoStorage)
+
+
+def _unit_hash(seed: int, scen: np.ndarray, agent: np.ndarray, stream: int) -> np.ndarray:
+    """Uniform [0, 1) from splitmix64 of (seed, global scenario, agent, stream): a scenario's mix
+    depends only on its global index, so every shard of a multi-GPU run draws it alone."""
+    with np.errstate(over='ignore'):
+        x = (np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + scen.astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9)
+             + agent.astype(np.uint64) * np.uint64(0x94D049BB133111EB) + np.uint64(stream) * np.uint64(0x2545F4914F6CDD1D))
+        for m, s in ((0xBF58476D1CE4E5B9, 30), (0x94D049BB133111EB, 27)):
+            x = (x ^ (x >> np.uint64(s))) * np.uint64(m)
+        x = x ^ (x >> np.uint64(31))
+    return (x >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+
+
+def asset_mix(S: int, N: int, first_scenario: int = 0, seed: int = setup.seed, p_no_pv: float = 0.2,
+              p_no_hp: float = 0.25, p_big_hp: float = 0.3, p_no_battery: float = 0.4,
+              battery_j: float = 10.0 * 3.6e6) -> AssetMix:
+    """PV-only / heat-pump / battery mixes for scenarios [first_scenario, first_scenario + S)."""
+    scen = np.arange(first_scenario, first_scenario + S)[:, None] + np.zeros((1, N), np.int64)
+    agent = np.zeros((S, 1), np.int64) + np.arange(N)[None, :]
+    has_pv = _unit_hash(seed, scen, agent, 1) >= p_no_pv
+    lv = np.broadcast_to(np.array([0.0, 1500.0, 3000.0], np.float32), (S, N, 3)).copy()
+    lv[_unit_hash(seed, scen, agent, 3) < p_big_hp] = np.array([0.0, 2500.0, 5000.0], np.float32)
+    lv[_unit_hash(seed, scen, agent, 2) < p_no_hp] = 0.0
+    cap = np.where(_unit_hash(seed, scen, agent, 4) < p_no_battery, 0.0, battery_j)
+    return AssetMix(has_pv=has_pv, hp_levels=lv, battery_capacity=cap)
+
+
+def apply_asset_mix(inp: ScenarioInputs, mix: AssetMix) -> ScenarioInputs:
+    """Consumers get a zero PV profile and max_in = load_kW * 1.1e3 (community.py:220's formula
+    with no PV rating)."""
+    pv_w = np.where(mix.has_pv[..., None], inp.pv_w, np.float32(0.0)).astype(np.float32)
+    max_in = np.where(mix.has_pv, inp.max_in,
+                      (np.asarray(inp.load_ratings) * 1.1 * 1e3).astype(np.float32)).astype(np.float32)
+    return ScenarioInputs(time=inp.time, t_out=inp.t_out, load_w=inp.load_w, pv_w=pv_w, max_in=max_in,
+                          t_in0=inp.t_in0, t_m0=inp.t_m0, load_ratings=inp.load_ratings,
+                          pv_ratings=np.where(mix.has_pv, inp.pv_ratings, 0.0))
