@@ -127,6 +127,7 @@ hipError_t launch_rule_episode(const EpisodeParams& p, float* hp_on, hipStream_t
 // shared table, N = 16, R <= 1 (configs[2]): episode_sq16_kernel; records packed like the fast path
 hipError_t launch_episode_sq16(const EpisodeParams& p, int q_dtype, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
 constexpr size_t kFastRecBytes = 32;  // one packed record row per agent-step (FastRec)
+constexpr int kFastBatMaxR1 = 2;      // episode_fast_kernel's battery variants: R + 1 <= 2
 // which: 0..4 reward, cost, grid, p2p, tin ([T][A] f32); 5 action (u8), 6 index (i32) [T][R+1][A]
 hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void* recs, int narrow, int which, void* out,
                                   hipStream_t stream);

@@ -929,8 +929,76 @@ __device__ __forceinline__ void gather_even(float ev, float (&col)[N], int i) {
   }
 }
 
-// episode_fast_kernel: episode_kernel's per-agent-table path (no battery, no shared table,
-// G <= 8, R + 1 <= 4, code words from a pre-pass) with the rounds unrolled at compile time and the
+// f64 division with a hoisted reciprocal: hipcc's IEEE f64 sequence (v_div_scale, v_rcp_f64, two
+// Newton steps, q = n * y, r = fma(-d, q, n), v_div_fmas = fma(r, y, q), v_div_fixup) with the
+// scale / fixup steps dropped, which is exact while |n| and |d| lie in [2^-300, 2^300] (the
+// exponent gap stays below the 768 where v_div_scale starts scaling); else the IEEE operator.
+struct Recip64 {
+  double d, y;
+  bool ok;
+};
+__device__ __forceinline__ bool in_div_range64(double x) {
+  const double m = fabs(x);
+  return m >= 0x1p-300 && m <= 0x1p300;
+}
+__device__ __forceinline__ Recip64 recip64(double d) {
+  const double r0 = __builtin_amdgcn_rcp(d);
+  const double r1 = __builtin_fma(r0, __builtin_fma(-d, r0, 1.0), r0);
+  return Recip64{d, __builtin_fma(r1, __builtin_fma(-d, r1, 1.0), r1), in_div_range64(d)};
+}
+__device__ __forceinline__ double fdiv64_ieee(double n, double d) {
+  asm volatile("" : "+v"(n));
+  return n / d;
+}
+__device__ __forceinline__ double fdiv64(double n, const Recip64& r) {
+  const double q = n * r.y;
+  double res = __builtin_fma(__builtin_fma(-r.d, q, n), r.y, q);
+  res = __builtin_copysign(res, q);  // +-0 / d keeps sign(n) * sign(d), as the IEEE quotient
+  if (!(r.ok && (n == 0.0 || in_div_range64(n)))) res = fdiv64_ieee(n, r.d);
+  return res;
+}
+// reciprocals of kernel-uniform divisors, moved to SGPRs (v_readfirstlane): VGPRs set the
+// occupancy of the throughput-bound sq16 kernel
+__device__ __forceinline__ float sgpr_f(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+__device__ __forceinline__ double sgpr_d(double x) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ Recip recip_u(float b) {
+  const Recip r = recip(b);
+  return Recip{b, sgpr_f(r.y), r.ok};
+}
+__device__ __forceinline__ Recip64 recip64_u(double d) {
+  const Recip64 r = recip64(d);
+  return Recip64{d, sgpr_d(r.y), r.ok};
+}
+// battery_rule (agent.py:138-153 + storage.py bookkeeping) with the divisions by the agent's
+// capacity, sqrt(efficiency) and 900 s through hoisted reciprocals; same op order, same results
+struct BatK {
+  double smin, smax, se;
+  Recip64 rse, r900;
+};
+__device__ __forceinline__ double battery_rule_r(double balance, double& soc, double cap, const Recip64& rcap,
+                                                 const BatK& b) {
+  const double energy = (balance * 60.0) * 15.0;
+  const double avail_energy = (fmax(0.0, soc - b.smin) * cap) * b.se;
+  const double avail_space = fdiv64(fmax(0.0, b.smax - soc) * cap, b.rse);
+  if (balance > 0.0 && avail_energy > 0.0) {
+    const double x = energy <= avail_energy ? energy : avail_energy;  // min(energy, available_energy)
+    soc = soc - fdiv64(fdiv64(x, rcap), b.rse);
+    balance = balance - fdiv64(x, b.r900);
+  } else if (balance < 0.0 && !(soc >= b.smax)) {
+    const double x = -energy <= avail_space ? -energy : avail_space;
+    soc = soc + b.se * fdiv64(x, rcap);
+    balance = balance + fdiv64(x, b.r900);
+  }
+  return balance;
+}
+
+// episode_fast_kernel: episode_kernel's per-agent-table path (no shared table, G <= 8,
+// R + 1 <= 4, or <= 2 with a battery, code words from a pre-pass) with the rounds unrolled at compile time and the
 // policy-independent per-step work (balance, time / balance bins, the next state's bins) read
 // from step_prepass_kernel's output.  Same op order, same results, bit for bit (tests compare
 // both kernels with the oracle).  Latency structure per step:
@@ -943,7 +1011,10 @@ __device__ __forceinline__ void gather_even(float ev, float (&col)[N], int i) {
 //     slot), so the number of memory ops behind each load is static and the loop-top wait for
 //     the prefetched rows is vmcnt(3), not a vmcnt(0) drain of the step's stores;
 //   * records go out as ONE 32-B row per agent-step (FastRec) and are unpacked on request;
-//   * division by max_in / 60 / N uses the hoisted reciprocal (fdiv above).
+//   * division by max_in / 60 / N uses the hoisted reciprocal (fdiv above);
+//   * BAT (configs[3] mixes): every round's net power goes through the battery rule first (f64,
+//     SoC committed by the final round, agent.py:138-153), with the capacity / sqrt(eff) / 900 s
+//     divisions through hoisted reciprocals (battery_rule_r); agents with capacity 0 skip it.
 // spw = scenarios per wave (<= 64 / G): fewer scenarios per wave spread the waves over more CUs.
 struct FastRec {         // [T][A], 32 B
   float reward, cost, grid, p2p, tin;
@@ -951,7 +1022,7 @@ struct FastRec {         // [T][A], 32 B
   uint32_t bins;         // (it * nT*nb + ib) | iT << 16
   uint32_t ips;          // byte r: p2p bin of round r
 };
-template <int N, typename QT, int R1, bool TRAIN>
+template <int N, typename QT, int R1, bool TRAIN, bool BAT>
 __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams p, const uint2* __restrict__ pre,
                                                              FastRec* __restrict__ recs, int spw, int n_cons,
                                                              const PrepOut nxt) {
@@ -967,7 +1038,8 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   static_assert(G <= 8 && R1 >= 1 && R1 <= 4, "fast path: G <= 8, R + 1 <= 4");
   // N = 2: round 1's Q row is one of three (by the partner's round-0 action) whose bins the
   // pre-pass wrote; all three are issued a step ahead, so round 1 waits for no gather
-  constexpr bool CAND = N == 2 && R1 >= 2;
+  // (not with a battery: the partner's round-0 power then depends on its state of charge)
+  constexpr bool CAND = N == 2 && R1 >= 2 && !BAT;
   const int lane = (int)threadIdx.x;
   const int sl = lane / G;
   const int i = lane % G;
@@ -989,6 +1061,15 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const float4 lv = p.hp_lv[a];
   float tin = active ? p.t_in[a] : k.setpoint;
   float tm = active ? p.t_m[a] : k.setpoint;
+  double bcap = 0.0, soc = 0.0;
+  BatK bk{};
+  Recip64 rcap{};
+  if constexpr (BAT) {
+    bcap = active ? p.bat_cap[a] : 0.0;
+    soc = active ? p.soc[a] : 0.0;
+    bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64_u(p.bat_sqrt_eff), recip64_u(900.0)};
+    rcap = recip64(bcap > 0.0 ? bcap : 1.0);
+  }
   const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, np);  // round 0 and next state: p2p = 0 (agent.py:203)
   // stores of inactive lanes (and every record when none is requested) go to a per-lane dummy slot
   QT* const q_dummy = reinterpret_cast<QT*>(p.dummy) + lane * kQPad;
@@ -1064,7 +1145,12 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     int ip = ip_zero;
     Row4<QT> rowR = row0;
     uint32_t acts = (uint32_t)act, ips = (uint32_t)ip_zero;
-    const float ev0 = div_n_r<N>((balw + hp) * 1.0f, rn);
+    float out0 = balw + hp;
+    double soc_r = soc;  // tentative SoC of the current round
+    if constexpr (BAT) {
+      if (bcap > 0.0) out0 = (float)battery_rule_r((double)out0, soc_r, bcap, rcap, bk);
+    }
+    const float ev0 = div_n_r<N>(out0 * 1.0f, rn);
 #pragma unroll
     for (int j = 0; j < N; ++j) row[j] = ev0;
     EnvRow e2;
@@ -1110,7 +1196,11 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       acts |= (uint32_t)act << (8 * r);
       ips |= (uint32_t)ip << (8 * r);
       hp = hp_of(lv, act);
-      const float out = balw + hp;
+      float out = balw + hp;
+      if constexpr (BAT) {
+        soc_r = soc;
+        if (bcap > 0.0) out = (float)battery_rule_r((double)out, soc_r, bcap, rcap, bk);
+      }
       // _divide_power's filter keeps pw where sign(out) != sign(pw) (agent.py:187-188): for out > 0
       // that is pw <= 0, for out < 0 pw >= 0, for out = 0 any pw.  A kept pw = +-0 and a dropped
       // one (0) are interchangeable: every later use is |f| or a sum that already holds +0.
@@ -1149,6 +1239,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       p2 = preb[o2];
       c2 = codes_a[o2];
     }
+    soc = soc_r;  // BatteryStorage state after the final round's decision
 
     // CommunityMicrogrid._step -> HPHeating.step (community.py:184-188, heating.py:138-143), then
     // the next step's rows are issued before this step's market work
@@ -1248,6 +1339,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       t0_draw(p.seed_lo, p.seed_hi, p.episode + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, tin, tm);
     p.t_in[a] = tin;
     p.t_m[a] = tm;
+    if constexpr (BAT) p.soc[a] = soc;
     if (i == 0) p.ep_reward[s] = ep_sum;
   }
 }
@@ -1282,15 +1374,23 @@ __global__ void fast_rec_unpack_kernel(int T, int R1, int A, uint32_t tb, const 
 
 // hipExtLaunchKernel stamps the start / stop events from the dispatch itself: no marker packets
 // between back-to-back episodes
+template <int N, typename QT, int R1, bool BAT>
+void launch_fast_b(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
+                   const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  if (p.mode == 0)
+    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, true, BAT>), dim3(blocks + prod), dim3(kWave), 0, st, ev0,
+                          ev1, 0, p, pre, recs, spw, blocks, nxt);
+  else
+    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, false, BAT>), dim3(blocks + prod), dim3(kWave), 0, st, ev0,
+                          ev1, 0, p, pre, recs, spw, blocks, nxt);
+}
 template <int N, typename QT, int R1>
 void launch_fast_r(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
                    const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
-  if (p.mode == 0)
-    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, true>), dim3(blocks + prod), dim3(kWave), 0, st, ev0, ev1, 0,
-                          p, pre, recs, spw, blocks, nxt);
-  else
-    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, false>), dim3(blocks + prod), dim3(kWave), 0, st, ev0, ev1,
-                          0, p, pre, recs, spw, blocks, nxt);
+  if constexpr (R1 <= kFastBatMaxR1) {
+    if (p.battery) return launch_fast_b<N, QT, R1, true>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
+  }
+  launch_fast_b<N, QT, R1, false>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
 }
 
 template <int N, typename QT>
@@ -1365,74 +1465,6 @@ __device__ __forceinline__ pkf2 fdiv_core_pk(pkf2 a, pkf2 b, pkf2 y) {
   r = __builtin_elementwise_fma(b, q1, -a);
   return __builtin_elementwise_fma(-r, y, q1);
 }
-// f64 division with a hoisted reciprocal: hipcc's IEEE f64 sequence (v_div_scale, v_rcp_f64, two
-// Newton steps, q = n * y, r = fma(-d, q, n), v_div_fmas = fma(r, y, q), v_div_fixup) with the
-// scale / fixup steps dropped, which is exact while |n| and |d| lie in [2^-300, 2^300] (the
-// exponent gap stays below the 768 where v_div_scale starts scaling); else the IEEE operator.
-struct Recip64 {
-  double d, y;
-  bool ok;
-};
-__device__ __forceinline__ bool in_div_range64(double x) {
-  const double m = fabs(x);
-  return m >= 0x1p-300 && m <= 0x1p300;
-}
-__device__ __forceinline__ Recip64 recip64(double d) {
-  const double r0 = __builtin_amdgcn_rcp(d);
-  const double r1 = __builtin_fma(r0, __builtin_fma(-d, r0, 1.0), r0);
-  return Recip64{d, __builtin_fma(r1, __builtin_fma(-d, r1, 1.0), r1), in_div_range64(d)};
-}
-__device__ __forceinline__ double fdiv64_ieee(double n, double d) {
-  asm volatile("" : "+v"(n));
-  return n / d;
-}
-__device__ __forceinline__ double fdiv64(double n, const Recip64& r) {
-  const double q = n * r.y;
-  double res = __builtin_fma(__builtin_fma(-r.d, q, n), r.y, q);
-  res = __builtin_copysign(res, q);  // +-0 / d keeps sign(n) * sign(d), as the IEEE quotient
-  if (!(r.ok && (n == 0.0 || in_div_range64(n)))) res = fdiv64_ieee(n, r.d);
-  return res;
-}
-// reciprocals of kernel-uniform divisors, moved to SGPRs (v_readfirstlane): VGPRs set the
-// occupancy of the throughput-bound sq16 kernel
-__device__ __forceinline__ float sgpr_f(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
-__device__ __forceinline__ double sgpr_d(double x) {
-  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-__device__ __forceinline__ Recip recip_u(float b) {
-  const Recip r = recip(b);
-  return Recip{b, sgpr_f(r.y), r.ok};
-}
-__device__ __forceinline__ Recip64 recip64_u(double d) {
-  const Recip64 r = recip64(d);
-  return Recip64{d, sgpr_d(r.y), r.ok};
-}
-// battery_rule (agent.py:138-153 + storage.py bookkeeping) with the divisions by the agent's
-// capacity, sqrt(efficiency) and 900 s through hoisted reciprocals; same op order, same results
-struct BatK {
-  double smin, smax, se;
-  Recip64 rse, r900;
-};
-__device__ __forceinline__ double battery_rule_r(double balance, double& soc, double cap, const Recip64& rcap,
-                                                 const BatK& b) {
-  const double energy = (balance * 60.0) * 15.0;
-  const double avail_energy = (fmax(0.0, soc - b.smin) * cap) * b.se;
-  const double avail_space = fdiv64(fmax(0.0, b.smax - soc) * cap, b.rse);
-  if (balance > 0.0 && avail_energy > 0.0) {
-    const double x = energy <= avail_energy ? energy : avail_energy;  // min(energy, available_energy)
-    soc = soc - fdiv64(fdiv64(x, rcap), b.rse);
-    balance = balance - fdiv64(x, b.r900);
-  } else if (balance < 0.0 && !(soc >= b.smax)) {
-    const double x = -energy <= avail_space ? -energy : avail_space;
-    soc = soc + b.se * fdiv64(x, rcap);
-    balance = balance + fdiv64(x, b.r900);
-  }
-  return balance;
-}
-
 // episode_sq16_kernel: episode_kernel's shared-table path for 16-agent scenarios (configs[2]),
 // rebuilt for throughput: 1M scenarios keep every SIMD busy, so the cost is instructions per
 // agent-step, not latency.  Same op order and results as episode_kernel (tests compare both).

@@ -628,7 +628,8 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   // fast per-agent-table path (episode_fast_kernel): automatic whenever it applies
   static const int env_spw = [] { const char* v = getenv("P2PMG_SPW"); return v ? atoi(v) : 0; }();
   static const bool env_general = [] { const char* v = getenv("P2PMG_KERNEL"); return v && !strcmp(v, "general"); }();
-  const bool fast = !g.shared_q && !c->battery && c->N <= 8 && c->R + 1 <= 4 && c->mi_ok &&
+  const bool fast = !g.shared_q && (!c->battery || c->R + 1 <= p2pmg::kFastBatMaxR1) && c->N <= 8 &&
+                    c->R + 1 <= 4 && c->mi_ok &&
                     (long long)g.n_time_states * g.n_temp_states * g.n_balance_states < 65536 &&
                     (long long)c->T * c->A < (1LL << 32) && host_div_range(g.minutes_per_hour) &&
                     host_div_range(g.temp_margin) &&
@@ -645,7 +646,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   if (fast) {
     const size_t ta = (size_t)c->T * c->A;
     const bool philox = train && args->rng == P2PMG_RNG_PHILOX;
-    const bool want_ipc = c->N == 2 && c->R >= 1;
+    const bool want_ipc = c->N == 2 && c->R >= 1 && !c->battery;  // the kernel's CAND path
     for (int k = 0; k < 2; ++k) {  // both slots (the launch writes the other one)
       if (!c->pre[k]) HIP_TRY(c, dmalloc(&c->pre[k], ta));
       if (want_ipc && !c->pre_ipc[k]) HIP_TRY(c, dmalloc(&c->pre_ipc[k], ta));
@@ -918,6 +919,7 @@ int p2pmg_set_hp_levels(p2pmg_ctx* c, const float* levels) {
 int p2pmg_set_battery(p2pmg_ctx* c, const double* capacity, double min_soc, double max_soc, double efficiency,
                       const double* soc0) {
   if (!c) return P2PMG_E_INVALID;
+  c->inputs_version++;  // the fast path's pre-pass writes the N = 2 round-1 bins only without a battery
   if (!capacity) {
     c->battery = false;
     return P2PMG_OK;

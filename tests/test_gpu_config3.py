@@ -62,6 +62,10 @@ def _cmp(out, rec, tag):
     (4, 2, 32, "f64", False, True, True),      # config 4 shape: per-agent tables, mixed assets
     (16, 1, 16, "f32", False, True, True),
     (2, 1, 96, "f64", False, False, True),
+    (4, 1, 48, "f64", False, True, True),      # configs[3] shape on the fast kernel (battery variant)
+    (2, 1, 96, "f64", False, True, True),      # N = 2 with a battery: no round-1 candidate rows
+    (3, 0, 24, "f32", False, True, True),
+    (8, 1, 24, "f32", False, True, False),
 ])
 def test_shared_battery_hetero_match_oracle(N, R, T, q_dtype, shared, battery, hetero):
     S = 24

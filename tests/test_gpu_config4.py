@@ -64,7 +64,7 @@ def test_year_episode_prefix_bit_exact_and_properties():
     gids = pick[:, None] * N + np.arange(N)[None, :]
     eng.run_episode("train", "philox", episode=0, epsilon=0.81, record=REC)
     rec = eng.get_records(REC)
-    assert eng.last_kernel().startswith("episode_kernel")
+    assert eng.last_kernel() == "episode_fast_kernel<4,f64,R1=2,train,battery>"
     out = ob.run_episode("train", rng="philox", episode=0, eps=0.81, agent_ids=gids)
     for k in ("reward", "cost", "grid", "p2p", "t_in"):
         assert np.array_equal(rec[k][:PREFIX, pick], out[k]), k
@@ -82,12 +82,33 @@ def test_year_episode_prefix_bit_exact_and_properties():
     # the P2P market clears bilaterally: what a scenario imports from peers, its peers export
     assert np.all(np.abs(rec["p2p"].sum(axis=-1)) <= 1e-3 * (1 + np.abs(rec["p2p"]).sum(axis=-1)))
     # a greedy year afterwards is deterministic: two runs agree bit-for-bit
-    t0 = eng.get_temperatures()
+    t0, soc0 = eng.get_temperatures(), eng.get_soc()
     eng.run_episode("greedy", record=("reward", "action"))
     g1 = eng.get_records(("reward", "action"))
     eng.set_temperatures(*t0)
-    eng.set_battery(mix.battery_capacity, 0.1, 0.9, 0.9)
+    eng.set_battery(mix.battery_capacity, 0.1, 0.9, 0.9, soc0=soc0)
     eng.run_episode("greedy", record=("reward", "action"))
     g2 = eng.get_records(("reward", "action"))
     assert all(np.array_equal(g1[k], g2[k]) for k in g1)
     eng.close()
+
+
+def test_year_fast_kernel_equals_general_kernel():
+    """The whole year, every scenario: the fast kernel's battery variant and the general
+    episode_kernel (in-kernel Philox draws) give the same records, SoC, temperatures and tables."""
+    S, N, R, T = 64, 4, 1, YEAR
+    inp, mix = _inputs(S, N, T, seed=7)
+    res = []
+    for kern, phil in (("auto", "auto"), ("general", "inkernel")):
+        eng = _device(inp, mix, S, N, R, T)
+        for e in range(2):
+            eng.run_episode("train", "philox", episode=e, epsilon=0.5, record=REC, kernel=kern, philox=phil)
+        res.append((eng.last_kernel(), eng.get_records(REC), eng.get_soc(), eng.get_temperatures(),
+                    eng.get_q(first=0, count=8)))
+        eng.close()
+    (k0, r0, s0, t0, q0), (k1, r1, s1, t1, q1) = res
+    assert k0.startswith("episode_fast_kernel") and k1.startswith("episode_kernel")
+    for k in REC:
+        assert np.array_equal(r0[k], r1[k]), k
+    assert np.array_equal(s0, s1) and np.array_equal(q0, q1)
+    assert all(np.array_equal(a, b) for a, b in zip(t0, t1))
