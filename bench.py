@@ -13,10 +13,10 @@ N GPUs: one process per GPU (torchrun), scenarios sharded with no data-path coll
 scenario's tables are private: "replicas only"); torch.distributed(gloo) carries only the
 barrier and the max-over-ranks time.  value = all ranks' agent-steps / max time (weak scaling).
 
-``--workload config4`` (BASELINE.json configs[3]): 4096 scenarios x 4 households per GPU with
+``--workload config4`` (BASELINE.json configs[3]): 8192 scenarios x 4 households per GPU with
 heterogeneous asset mixes (dataset.asset_mix: Consumers without PV, no / 3 kW / 5 kW heat pumps,
 10 kWh battery or NoStorage), one-year episodes (T = 35,040 quarter-hour slots), per-agent f64
-Q-tables (84 GB per GPU): replicas only, like configs[1].
+Q-tables (168 GB per GPU, sized to HBM): replicas only, like configs[1].
 
 ``--workload config3`` (BASELINE.json configs[2]): 1M scenarios x 16 agents with battery storage
 over 8 GPUs = 125,000 scenarios (2M agents) per GPU, ONE shared f32 Q-table whose int64
@@ -101,7 +101,7 @@ WORKLOADS = {
     "config3": (125000, 16, 1, 96, "f32", True, True),
     "config5": (4096, 2, 1, 96, "f32", True, False),  # DQN, one shared network (data-parallel)
     # configs[3]: heterogeneous PV / heat-pump / battery mixes, 1-year episodes, per-agent tables
-    "config4": (4096, 4, 1, 365 * 96, "f64", False, True),
+    "config4": (8192, 4, 1, 365 * 96, "f64", False, True),  # 32,768 f64 tables = 168 GB of HBM
 }
 HETERO = {"config4"}
 

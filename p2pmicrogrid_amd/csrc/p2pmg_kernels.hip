@@ -975,26 +975,44 @@ __device__ __forceinline__ Recip64 recip64_u(double d) {
   return Recip64{d, sgpr_d(r.y), r.ok};
 }
 // battery_rule (agent.py:138-153 + storage.py bookkeeping) with the divisions by the agent's
-// capacity, sqrt(efficiency) and 900 s through hoisted reciprocals; same op order, same results
+// capacity, sqrt(efficiency) and 900 s through hoisted reciprocals; same op order, same results.
+// Branch-free: the discharge and charge branches divide the same expressions of their own x, so x
+// is selected first and x / cap, x / 900, (x / cap) / sqrt(eff) are computed once (4 quotients
+// instead of up to 6 on a divergent wave); one range test for all of them, and a lane with an
+// operand outside the range-free quotient's domain redoes the rule with IEEE divisions.
 struct BatK {
   double smin, smax, se;
   Recip64 rse, r900;
 };
+// 0, or |n| in [2^-300, 2^300) by its biased exponent (723..1322): the range-free quotient's domain
+__device__ __forceinline__ bool q64_ok(double n) {
+  const unsigned e = ((unsigned)__double2hiint(n) >> 20) & 0x7FFu;
+  return (e - 723u <= 599u) || n == 0.0;
+}
+// fdiv64 without its range test (the caller tests the operands)
+__device__ __forceinline__ double qcore64(double n, const Recip64& r) {
+  const double q = n * r.y;
+  return __builtin_copysign(__builtin_fma(__builtin_fma(-r.d, q, n), r.y, q), q);
+}
 __device__ __forceinline__ double battery_rule_r(double balance, double& soc, double cap, const Recip64& rcap,
                                                  const BatK& b) {
   const double energy = (balance * 60.0) * 15.0;
   const double avail_energy = (fmax(0.0, soc - b.smin) * cap) * b.se;
-  const double avail_space = fdiv64(fmax(0.0, b.smax - soc) * cap, b.rse);
-  if (balance > 0.0 && avail_energy > 0.0) {
-    const double x = energy <= avail_energy ? energy : avail_energy;  // min(energy, available_energy)
-    soc = soc - fdiv64(fdiv64(x, rcap), b.rse);
-    balance = balance - fdiv64(x, b.r900);
-  } else if (balance < 0.0 && !(soc >= b.smax)) {
-    const double x = -energy <= avail_space ? -energy : avail_space;
-    soc = soc + b.se * fdiv64(x, rcap);
-    balance = balance + fdiv64(x, b.r900);
-  }
-  return balance;
+  const double space_n = fmax(0.0, b.smax - soc) * cap;
+  const double avail_space = qcore64(space_n, b.rse);
+  const bool dis = balance > 0.0 && avail_energy > 0.0;
+  const bool chg = !dis && balance < 0.0 && !(soc >= b.smax);
+  const double x = dis ? (energy <= avail_energy ? energy : avail_energy)    // min(energy, available_energy)
+                       : (-energy <= avail_space ? -energy : avail_space);  // min(-energy, available_space)
+  const double q1 = qcore64(x, rcap);     // x / capacity
+  const double q2 = qcore64(x, b.r900);   // x / 900
+  const double q3 = qcore64(q1, b.rse);   // (x / capacity) / sqrt(eff)
+  const bool ok = rcap.ok && b.rse.ok && b.r900.ok && q64_ok(x) && q64_ok(q1) && (!chg || q64_ok(space_n));
+  if ((dis || chg) && !ok) return battery_rule(balance, soc, cap, b.smin, b.smax, b.se);  // IEEE divisions
+  const double soc_n = dis ? soc - q3 : soc + b.se * q1;
+  const double bal_n = dis ? balance - q2 : balance + q2;
+  soc = (dis || chg) ? soc_n : soc;
+  return (dis || chg) ? bal_n : balance;
 }
 
 // episode_fast_kernel: episode_kernel's per-agent-table path (no shared table, G <= 8,
