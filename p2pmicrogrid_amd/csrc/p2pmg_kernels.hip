@@ -1163,6 +1163,34 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     int ip = ip_zero;
     Row4<QT> rowR = row0;
     uint32_t acts = (uint32_t)act, ips = (uint32_t)ip_zero;
+    // CommunityMicrogrid._step -> HPHeating.step (community.py:184-188, heating.py:138-143) needs
+    // only the final round's heat-pump power: it and the next step's row gathers are issued as soon
+    // as that is known, ahead of the final round's divide-power and this step's market work
+    float tin1 = tin, tm1 = tm;
+    int iT1 = 0;
+    uint32_t strip1 = 0, cw1 = 0, a0n = 0, aNn = 0;
+    Row4<QT> row0n, rowNn, candn[3];
+    auto issue_next = [&](float hp_final) {
+      rc_update(k, e0.t_out, hp_final, tin1, tm1);
+      iT1 = temp_bin(tin1);
+      strip1 = strip_of(p1.y & 0xFFFFu, iT1);
+      const uint32_t nrow1 = strip_of(p1.y >> 16, iT1) + (uint32_t)ip_zero;
+      cw1 = code_of(c1);
+      a0n = row0_addr(strip1, nrow1, cw1);
+      aNn = TRAIN ? nrow1 : a0n;
+#if P2PMG_ABLATE == 8
+      row0n = fake_row(q + a0n * kQPad);
+      rowNn = fake_row(q + aNn * kQPad);
+#else
+      row0n = gather_row(q + a0n * kQPad);
+      rowNn = gather_row(q + aNn * kQPad);
+#endif
+      if constexpr (CAND) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) candn[b] = gather_row(q + (strip1 + ((ipc1 >> (8 * b)) & 0xFFu)) * kQPad);
+      }
+    };
+    if constexpr (R1 == 1) issue_next(hp);
     float out0 = balw + hp;
     double soc_r = soc;  // tentative SoC of the current round
     if constexpr (BAT) {
@@ -1214,6 +1242,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       acts |= (uint32_t)act << (8 * r);
       ips |= (uint32_t)ip << (8 * r);
       hp = hp_of(lv, act);
+      if (r == R1 - 1) issue_next(hp);
       float out = balw + hp;
       if constexpr (BAT) {
         soc_r = soc;
@@ -1258,30 +1287,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       c2 = codes_a[o2];
     }
     soc = soc_r;  // BatteryStorage state after the final round's decision
-
-    // CommunityMicrogrid._step -> HPHeating.step (community.py:184-188, heating.py:138-143), then
-    // the next step's rows are issued before this step's market work
-    float tin1 = tin, tm1 = tm;
-    rc_update(k, e0.t_out, hp, tin1, tm1);
-    const int iT1 = temp_bin(tin1);
-    const uint32_t strip1 = strip_of(p1.y & 0xFFFFu, iT1);
-    const uint32_t nrow1 = strip_of(p1.y >> 16, iT1) + (uint32_t)ip_zero;
-    const uint32_t cw1 = code_of(c1);
-    const uint32_t a0n = row0_addr(strip1, nrow1, cw1);
-    const uint32_t aNn = TRAIN ? nrow1 : a0n;
-#if P2PMG_ABLATE == 8
-    const Row4<QT> row0n = fake_row(q + a0n * kQPad);
-    const Row4<QT> rowNn = fake_row(q + aNn * kQPad);
-#else
-    const Row4<QT> row0n = gather_row(q + a0n * kQPad);
-    const Row4<QT> rowNn = gather_row(q + aNn * kQPad);
-#endif
-    Row4<QT> candn[3];
-    if constexpr (CAND) {
-#pragma unroll
-      for (int b = 0; b < 3; ++b) candn[b] = gather_row(q + (strip1 + ((ipc1 >> (8 * b)) & 0xFFu)) * kQPad);
-    }
-    pat.row = 0xFFFFFFFFu;
+    pat.row = 0xFFFFFFFFu;  // the next step's rows were issued after the previous TD store
 
     // CommunityMicrogrid._assign_powers community.py:45-54 on the final P (diagonal kept)
     exchange<N>(row, col, i, sl, nullptr);
