@@ -547,14 +547,30 @@ __global__ void dqn_reduce_chunks_kernel(const DqnParams d, int n_partials, int 
   const int b1 = min(n_partials, b0 + per);
   float* g = d.grad + k;
   float s = 0.0f;
-  for (int b = b0; b < b1; ++b) s += g[(size_t)b * kNetStride];
+  int b = b0;
+  for (; b + 8 <= b1; b += 8) {  // 8 loads in flight, the sum still in partial order
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = g[(size_t)(b + u) * kNetStride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; b < b1; ++b) s += g[(size_t)b * kNetStride];
   g[(size_t)b0 * kNetStride] = s;
 }
 __global__ void dqn_reduce_kernel(const DqnParams d, int n_partials, int per) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= kDqnParams) return;
   float s = 0.0f;
-  for (int b = 0; b < n_partials; b += per) s += d.grad[(size_t)b * kNetStride + k];
+  int b = 0;
+  for (; b + 8 * per <= n_partials; b += 8 * per) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = d.grad[(size_t)(b + u * per) * kNetStride + k];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; b < n_partials; b += per) s += d.grad[(size_t)b * kNetStride + k];
   d.gsum[k] = s;
 }
 
