@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
 }
 
 // the weights one train workgroup reads, per lane (wave w owns columns 16w..16w+15)
-// (W2 itself is read per MFMA step from L1/L2: held in registers it costs the second wave per SIMD)
+// (per-agent networks read W2 per MFMA step from L1/L2; a shared network stages it in LDS)
 struct TrainW {
   float bt0, bo0, bt1, bo1, b1t, b1o, b2t, w3t, b2o, w3o, b3t, b3o;
 };
@@ -303,6 +303,8 @@ __device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const f
   W.b3o = th[kOffB3];
 }
 
+__device__ __forceinline__ int w2_swz(int k) { return ((k & 3) << 4) | (((k >> 2) & 3) << 2); }
+
 template <bool SHARED>
 __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) {  // 2 waves / SIMD
   __shared__ float smpb[2][kB * kTrans];  // this agent's batch and the next one's (prefetched)
@@ -310,6 +312,10 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   __shared__ float H1o[kB][kLdsRow];
   __shared__ float dZ2[kB][kLdsRow];
   __shared__ float qpart[4][4 * kB];  // per-wave partial Q: rows 0..95 target (action x sample), 96..127 online
+  // one shared network: W2 (target, online) staged in LDS once per workgroup, element (k, j) at
+  // k*64 + (j ^ w2_swz(k)), conflict-free both for the forward's B operand (row k = 4 kk + g4,
+  // column j = col) and for dH1's W2^T read (row k = col, column j = 4 kk + g4)
+  __shared__ float W2s[SHARED ? 2 : 1][SHARED ? kH * kH : 1];
   const EpisodeParams& p = d.e;
   const int w = threadIdx.x / kWave, l = threadIdx.x % kWave;
   const int c16 = l & 15, g4 = l >> 4;
@@ -324,7 +330,16 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   const int n_ag = d.batch ? 1 : d.apb;
   int net = d.batch ? d.net : 0;
   TrainW W;
-  if (SHARED) load_train_w(W, d.theta + (size_t)net * kNetStride, d.target + (size_t)net * kNetStride, col, g4);
+  if constexpr (SHARED) {
+    const float* th0 = d.theta + (size_t)net * kNetStride;
+    const float* tg0 = d.target + (size_t)net * kNetStride;
+    load_train_w(W, th0, tg0, col, g4);
+    for (int e = threadIdx.x; e < kH * kH; e += 256) {
+      const int k = e / kH, j = e % kH;
+      W2s[0][k * kH + (j ^ w2_swz(k))] = tg0[kOffW2 + e];
+      W2s[SHARED ? 1 : 0][k * kH + (j ^ w2_swz(k))] = th0[kOffW2 + e];
+    }
+  }
   // the first agent's batch (explicit batch, or the sample pre-pass output)
   {
     const float* src = d.batch ? d.batch : d.smp + (size_t)blockIdx.x * d.apb * (kB * kTrans);
@@ -386,7 +401,8 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const int k = 4 * kk + g4;
-      const float bt = tg[kOffW2 + k * kH + col], bo = th[kOffW2 + k * kH + col];
+      const float bt = SHARED ? W2s[0][k * kH + (col ^ w2_swz(k))] : tg[kOffW2 + k * kH + col];
+      const float bo = SHARED ? W2s[SHARED ? 1 : 0][k * kH + (col ^ w2_swz(k))] : th[kOffW2 + k * kH + col];
 #pragma unroll
       for (int rt = 0; rt < 6; ++rt) at[rt] = mfma4(H1t[16 * rt + c16][k], bt, at[rt]);
       ao[0] = mfma4(H1o[c16][k], bo, ao[0]);
@@ -474,7 +490,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
 #pragma unroll
       for (int kk = 0; kk < 16; ++kk) {
         const int j = 4 * kk + g4;
-        acc = mfma4(dZ2[16 * rt + c16][j], th[kOffW2 + col * kH + j], acc);
+        acc = mfma4(dZ2[16 * rt + c16][j], SHARED ? W2s[SHARED ? 1 : 0][col * kH + (j ^ w2_swz(col))] : th[kOffW2 + col * kH + j], acc);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
