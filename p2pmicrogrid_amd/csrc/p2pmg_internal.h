@@ -52,7 +52,7 @@ struct EpisodeParams {
   void* dummy;               // >= 2 * kWave * 32 B scratch: target of the fast kernel's masked-off stores
   uint32_t* pre_ipc;         // fast path, N = 2: [T][A] round-1 p2p bins for the partner's 3 round-0 actions
   void* rec_pack;            // fast paths: packed records [T][A] x 32 B
-  int rec_narrow;            // sq16: only reward + cost requested -> rec_pack is [T][A] float2
+  int rec_narrow;            // fast / sq16: only reward + cost requested -> records are [T][A] float2
   int reset_t0;              // fast path: draw T0 for episode + 1 at the end (P2PMG_FLAG_RESET_T0)
   double reset_sigma;
   int nt, nT, nb, np;

@@ -1028,7 +1028,8 @@ __device__ __forceinline__ double battery_rule_r(double balance, double& soc, do
 //   * every store is unconditional (inactive lanes and disabled records write a per-lane dummy
 //     slot), so the number of memory ops behind each load is static and the loop-top wait for
 //     the prefetched rows is vmcnt(3), not a vmcnt(0) drain of the step's stores;
-//   * records go out as ONE 32-B row per agent-step (FastRec) and are unpacked on request;
+//   * records go out as ONE 32-B row per agent-step (FastRec), or as an 8-B {reward, cost} row
+//     when only those are requested, and are unpacked on request;
 //   * division by max_in / 60 / N uses the hoisted reciprocal (fdiv above);
 //   * BAT (configs[3] mixes): every round's net power goes through the battery rule first (f64,
 //     SoC committed by the final round, agent.py:138-153), with the capacity / sqrt(eff) / 900 s
@@ -1091,10 +1092,14 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, np);  // round 0 and next state: p2p = 0 (agent.py:203)
   // stores of inactive lanes (and every record when none is requested) go to a per-lane dummy slot
   QT* const q_dummy = reinterpret_cast<QT*>(p.dummy) + lane * kQPad;
-  FastRec* const rec_dummy = reinterpret_cast<FastRec*>(p.dummy) + kWave + lane;
+  // records: FastRec rows, or only {reward, cost} as float2 when nothing else was requested
+  // (not in the battery variant: its loop measured 2 % slower with the extra branch)
+  const bool narrow = !BAT && p.rec_narrow != 0;
+  const size_t rec_bytes = narrow ? sizeof(float2) : sizeof(FastRec);
+  char* const rec_dummy = reinterpret_cast<char*>(reinterpret_cast<FastRec*>(p.dummy) + kWave + lane);
   const bool rec_on = p.record != 0 && active;
-  FastRec* rec_ptr = rec_on ? recs + a : rec_dummy;
-  const size_t rec_step = rec_on ? A : 0;
+  char* rec_ptr = rec_on ? reinterpret_cast<char*>(recs) + (size_t)a * rec_bytes : rec_dummy;
+  const size_t rec_step = rec_on ? A * rec_bytes : 0;
 
   auto temp_bin = [&](float t_in) {  // idx_temp((T_in - setpoint) / margin) heating.py:118-120, rl.py:93
     const float dt = t_in - k.setpoint;
@@ -1322,13 +1327,15 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       *(active ? q + srow * kQPad + act : q_dummy) = qnew;
       pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
     }
-    {
+    if (narrow) {  // wave-uniform
+      *reinterpret_cast<float2*>(rec_ptr) = make_float2(rw, cost);
+    } else {
       const uint32_t bins = (p0.y & 0xFFFFu) | ((uint32_t)iT << 16);  // it * nT*nb + ib | iT << 16
       float4* rp = reinterpret_cast<float4*>(rec_ptr);
       rp[0] = make_float4(rw, cost, g, pp);
       rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
-      rec_ptr += rec_step;
     }
+    rec_ptr += rec_step;
     // avg_reward = sum_t mean_i r (community.py:179), canonical sequential order
     const float m = group_sum<N>(rw, lane, i, sl, nullptr);
     ep_sum = ep_sum + div_n_r<N>(m, rn);

@@ -61,7 +61,7 @@ struct p2pmg_ctx {
   void* dummy = nullptr;      // fast path: target of masked-off stores (2 * 64 * 32 B)
   void* rec_pack = nullptr;   // fast path: packed records [T][A] x 32 B
   int rec_fast_mask = 0;      // records of the last episode that live (packed) in rec_pack
-  int rec_narrow = 0;         // ... as [T][A] float2 {reward, cost} (sq16 with only those two requested)
+  int rec_narrow = 0;         // ... as [T][A] float2 {reward, cost} (fast / sq16 with only those two requested)
   int code_src = 0;          // what the code buffer holds: 0 none, 1 replay upload, 2 Philox pre-pass
   float* ep_reward = nullptr;
   float* rec_f32[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // reward, cost, grid, p2p, tin
@@ -696,8 +696,9 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     if (args->record && !c->rec_pack)
       HIP_TRY(c, hipMalloc(&c->rec_pack, (size_t)c->T * c->A * p2pmg::kFastRecBytes));
     p.rec_pack = c->rec_pack;
-    p.rec_narrow = (args->record & ~(P2PMG_REC_REWARD | P2PMG_REC_COST)) == 0 ? 1 : 0;
   }
+  // fast (without battery) / sq16: only {reward, cost} requested -> 8-B record rows
+  p.rec_narrow = ((fast && !p.battery) || sq16) && (args->record & ~(P2PMG_REC_REWARD | P2PMG_REC_COST)) == 0 ? 1 : 0;
   const bool ext = fast || sq16;  // launches that stamp their own timing events
   if (!ext) HIP_TRY(c, hipEventRecord(r0, c->stream));
   int spw = args->scen_per_wave > 0 ? args->scen_per_wave : env_spw;
@@ -716,7 +717,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
                         : p2pmg::launch_episode(p, g.q_dtype, c->stream);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));
   c->rec_fast_mask = ext ? (args->record & 127) : 0;
-  c->rec_narrow = sq16 ? p.rec_narrow : 0;
+  c->rec_narrow = (fast || sq16) ? p.rec_narrow : 0;
   c->last_kernel = std::string(fast ? "episode_fast_kernel<" : sq16 ? "episode_sq16_kernel<" : "episode_kernel<") +
                    std::to_string(c->N) + "," + (g.q_dtype == 0 ? "f64" : "f32") + ",R1=" + std::to_string(c->R + 1) +
                    (ext ? (train ? ",train" : ",greedy") : "") + (g.shared_q ? ",shared" : "") +
