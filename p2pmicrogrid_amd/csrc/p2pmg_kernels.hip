@@ -1151,8 +1151,10 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   float ep_sum = 0.0f;
   __builtin_amdgcn_s_waitcnt(0);  // enter the loop with nothing in flight (static waits inside)
 
-#pragma unroll 2
-  for (int t = 0; t < T; ++t) {
+  // one step; the loop below runs it twice per iteration (a manual unroll: the DPP exchanges are
+  // convergent, so the compiler will not unroll a loop with a runtime trip count), which lets the
+  // register allocator alternate the prefetched rows' registers instead of copying them
+  auto step = [&]() __attribute__((always_inline)) {
     const float balw = __uint_as_float(p0.x);
     float row[N];
     float col[N];
@@ -1364,7 +1366,13 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
 #pragma unroll
       for (int b = 0; b < 3; ++b) cand[b] = candn[b];
     }
+  };
+  int t = 0;
+  for (; t + 2 <= T; t += 2) {
+    step();
+    step();
   }
+  if (t < T) step();
   if (active) {
     if (p.reset_t0)  // agent.reset() at the end of train_episode (community.py:181), fused
       t0_draw(p.seed_lo, p.seed_hi, p.episode + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, tin, tm);
