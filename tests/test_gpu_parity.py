@@ -264,3 +264,28 @@ def test_fused_t0_reset_equals_separate_reset(kernel):
     assert np.array_equal(a.get_record("reward"), b.get_record("reward"))
     assert np.array_equal(a.episode_reward(), b.episode_reward())
     assert np.array_equal(a.get_q(), b.get_q())
+
+
+@pytest.mark.parametrize("N", [2, 4])
+def test_narrow_reward_cost_records_match_oracle(N):
+    """Only {reward, cost} requested: the fast kernel writes 8-B record rows instead of 32-B
+    FastRec rows.  Alternating narrow and full requests over back-to-back episodes, every
+    returned record still equals the oracle's."""
+    S, R, T = 80, 1, 48
+    inp = scenario_batch(S, N, T, seed=17)
+    ob = _oracle_for(inp, N, R)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = _device_for(inp, N, R)
+    for e in range(4):
+        narrow = e % 2 == 0
+        rec = ("reward", "cost") if narrow else REC
+        eng.run_episode("train", "philox", episode=e, epsilon=0.5, record=rec)
+        assert eng.last_kernel().startswith("episode_fast_kernel<")
+        out = ob.run_episode("train", rng="philox", seed=42, episode=e, eps=0.5)
+        got = eng.get_records(rec)
+        if not narrow:
+            _compare(out, got, e)
+        else:
+            assert np.array_equal(got["reward"], out["reward"]) and np.array_equal(got["cost"], out["cost"]), e
+        assert np.array_equal(eng.episode_reward(), out["episode_reward"]), e
+    assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
