@@ -332,6 +332,9 @@ def main():
         episode(e)
     eng.sync()
     eng.reset_kernel_times()
+    # HIP events on every launch cost ~4 us per configs[1] episode: sample every 5th launch
+    timing_period = 5 if args.steps >= 20 else 1
+    eng.set_timing_period(timing_period)
     barrier(world)
     eng.sync()
     t0 = time.perf_counter()
@@ -391,7 +394,7 @@ def main():
                          "kernel_ms": kernel_ms,
                          "algorithmic_bytes_per_agent_step": bpa,
                          "algorithmic_bytes_per_launch": bpa * steps_per_episode,
-                         "timed_launches": int(len(kms))},
+                         "timed_launches": int(len(kms)), "timing_period": timing_period},
             "mean_episode_reward": ep_reward,
         }
         if traffic:

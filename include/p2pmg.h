@@ -189,6 +189,10 @@ int p2pmg_last_kernel_ms(p2pmg_ctx* ctx, float* ms);           /* HIP-event time
  * (ring of the last 4096 launches, on the context's stream); *count = entries written. */
 int p2pmg_kernel_times(p2pmg_ctx* ctx, float* ms, int max, int* count);
 int p2pmg_reset_kernel_times(p2pmg_ctx* ctx);
+/* Stamp the episode kernel's timing events on every period-th episode launch only (default 1 =
+ * every launch; the counter restarts here and at p2pmg_reset_kernel_times, so the next launch is
+ * timed).  Timing-only: results do not depend on it. */
+int p2pmg_set_timing_period(p2pmg_ctx* ctx, int period);
 
 /* batched primitives (device) for unit parity against the reference functions */
 int p2pmg_rc_step(p2pmg_ctx* ctx, int n, const float* t_out, const float* t_in, const float* t_m,

@@ -273,6 +273,10 @@ class DeviceCommunityBatch:
     def reset_kernel_times(self):
         self._chk(self.L.p2pmg_reset_kernel_times(self._ctx), "reset_kernel_times")
 
+    def set_timing_period(self, period: int):
+        """Stamp timing events on every period-th episode launch only (timing-only setting)."""
+        self._chk(self.L.p2pmg_set_timing_period(self._ctx, int(period)), "set_timing_period")
+
     def get_record(self, name: str) -> np.ndarray:
         """[T, S, N] for per-step records, [T, R+1, S, N] for action/index."""
         bit = _lib.REC[name]

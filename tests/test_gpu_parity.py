@@ -289,3 +289,19 @@ def test_narrow_reward_cost_records_match_oracle(N):
             assert np.array_equal(got["reward"], out["reward"]) and np.array_equal(got["cost"], out["cost"]), e
         assert np.array_equal(eng.episode_reward(), out["episode_reward"]), e
     assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
+
+
+def test_timing_period_samples_launches_only():
+    """set_timing_period(k): only every k-th episode launch carries timing events; results are
+    the same as with every launch timed."""
+    S, N, R, T = 32, 2, 1, 24
+    inp = scenario_batch(S, N, T, seed=5)
+    a, b = _device_for(inp, N, R), _device_for(inp, N, R)
+    a.set_timing_period(3)
+    for e in range(7):
+        for eng in (a, b):
+            eng.run_episode("train", "philox", episode=e, epsilon=0.5, record=("reward", "cost"), reset_sigma=0.3)
+    assert len(a.kernel_times()) == 3 and len(b.kernel_times()) == 7
+    assert all(t > 0 for t in a.kernel_times())
+    assert np.array_equal(a.get_record("reward"), b.get_record("reward"))
+    assert np.array_equal(a.get_q(), b.get_q())
