@@ -249,9 +249,9 @@ __device__ __forceinline__ void adam_update(const DqnParams& d, float* th, float
 
 // ReplayBuffer.sample_batch rl.py:226-241 for every agent of the step, ahead of the train kernel:
 // one wave per agent draws 32 distinct deque indices (replayed, or Philox + Floyd as in
-// oracle/philox.py::sample_draws) and gathers the 32 transitions into d.smp [A][32][kTrans], so
-// the train kernel reads one contiguous 1280-B block per agent instead of waiting on 32 random
-// ring reads behind a serial 32-step selection loop.
+// oracle/philox.py::sample_draws) and writes their ring slots to d.smp (as int32 [A][32]); the
+// train kernel gathers each agent's 32 transitions from the ring one agent ahead (double-buffered),
+// so neither kernel waits on the random ring reads behind the serial 32-step selection loop.
 __global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
   const EpisodeParams& p = d.e;
   const int a = blockIdx.x, l = threadIdx.x;
@@ -275,12 +275,22 @@ __global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
       if (l == j) idx = taken ? count - kB + j : r;
     }
   }
-  if (l < kB) {
-    const float* src = d.buf + ((size_t)a * d.cap + (size_t)((first + idx) % d.cap)) * kTrans;
-    float* dst = d.smp + ((size_t)a * kB + l) * kTrans;
-#pragma unroll
-    for (int k = 0; k < kTrans; ++k) dst[k] = src[k];
-  }
+  if (l < kB) reinterpret_cast<int*>(d.smp)[(size_t)a * kB + l] = (first + idx) % d.cap;
+}
+
+// one thread's share of agent a's sampled batch (thread t: sample t / 8, floats t % 8 and, for
+// t % 8 < 2, t % 8 + 8), gathered from the replay ring through the sample kernel's slot indices
+__device__ __forceinline__ void batch_part(const DqnParams& d, int a, int t, float& v0, float& v1) {
+  const int b = t >> 3, k = t & 7;
+  const int slot = reinterpret_cast<const int*>(d.smp)[(size_t)a * kB + b];
+  const float* src = d.buf + ((size_t)a * d.cap + (size_t)slot) * kTrans;
+  v0 = src[k];
+  v1 = k < kTrans - 8 ? src[k + 8] : 0.0f;
+}
+__device__ __forceinline__ void batch_put(float* dst, int t, float v0, float v1) {
+  const int b = t >> 3, k = t & 7;
+  dst[b * kTrans + k] = v0;
+  if (k < kTrans - 8) dst[b * kTrans + k + 8] = v1;
 }
 
 // the weights one train workgroup reads, per lane (wave w owns columns 16w..16w+15)
@@ -341,10 +351,13 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     }
   }
   // the first agent's batch (explicit batch, or the sample pre-pass output)
-  {
-    const float* src = d.batch ? d.batch : d.smp + (size_t)blockIdx.x * d.apb * (kB * kTrans);
-    const bool ok = d.batch || (size_t)blockIdx.x * d.apb < A;
-    for (int k = threadIdx.x; k < kB * kTrans; k += 256) smpb[0][k] = ok ? src[k] : 0.0f;
+  if (d.batch) {
+    for (int k = threadIdx.x; k < kB * kTrans; k += 256) smpb[0][k] = d.batch[k];
+  } else {
+    const int a0 = blockIdx.x * d.apb;
+    float v0 = 0.0f, v1 = 0.0f;
+    if ((size_t)a0 < A) batch_part(d, a0, threadIdx.x, v0, v1);
+    batch_put(smpb[0], threadIdx.x, v0, v1);
   }
   __syncthreads();
 
@@ -359,11 +372,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     // prefetch the next agent's batch into registers; it goes to the other buffer at the end
     const bool has_next = !d.batch && ag + 1 < n_ag && a + 1 < (int)A;
     float nx0 = 0.0f, nx1 = 0.0f;
-    if (has_next) {
-      const float* src = d.smp + (size_t)(a + 1) * (kB * kTrans);
-      nx0 = src[threadIdx.x];
-      if (threadIdx.x < kB * kTrans - 256) nx1 = src[256 + threadIdx.x];
-    }
+    if (has_next) batch_part(d, a + 1, threadIdx.x, nx0, nx1);
 
     // ---- layer 1 (K = 5 padded to 8): Z1 = X W1 + b1, 6 target + 2 online row tiles
     const float bt0 = W.bt0, bo0 = W.bo0, bt1 = W.bt1, bo1 = W.bo1, b1t = W.b1t, b1o = W.b1o;
@@ -501,10 +510,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
         gW1 = mfma4(x, dz1, gW1);
       }
     }
-    if (has_next) {
-      smpb[(ag + 1) & 1][threadIdx.x] = nx0;
-      if (threadIdx.x < kB * kTrans - 256) smpb[(ag + 1) & 1][256 + threadIdx.x] = nx1;
-    }
+    if (has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
     __syncthreads();  // every wave is done with this agent's LDS and with the online W2
   }
 

@@ -85,7 +85,7 @@ struct DqnParams {
   int32_t* added;            // [A] transitions ever added
   int cap;
   const uint16_t* samples;   // replay mode: [T][A][32] deque indices; null = Philox (Floyd)
-  float* smp;                // [A][32][kTrans] this step's sampled transitions (dqn_sample_kernel)
+  float* smp;                // this step's sampled ring slots, int32 [A][32] (dqn_sample_kernel)
   float* rec_loss;           // [T][A] or null
   float* ep_acc;             // [S] running sum_t mean_i r
   float gamma, tau, tau_c, lr_t, b1c, b2c, adam_eps, clip;

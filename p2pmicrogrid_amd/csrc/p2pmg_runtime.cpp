@@ -89,7 +89,7 @@ struct p2pmg_ctx {
   float* d_v = nullptr;
   float* d_grad = nullptr;    // shared network: [d_blocks][kNetStride] partials
   float* d_gsum = nullptr;    // [kNetStride]
-  float* d_smp = nullptr;     // [A][32][kTrans] sampled batches of the current step
+  float* d_smp = nullptr;     // [A][32] int32 ring slots sampled for the current step
   int d_blocks = 0, d_apb = 1;
   float* d_buf = nullptr;     // [A][capacity][10]
   int32_t* d_added = nullptr; // [A]
@@ -1162,7 +1162,7 @@ int p2pmg_dqn_setup(p2pmg_ctx* c, const p2pmg_dqn_config* cfg) {
   }
   HIP_TRY(c, dmalloc(&c->d_buf, A * (size_t)cfg->capacity * p2pmg::kTrans));
   HIP_TRY(c, dmalloc(&c->d_added, A));
-  HIP_TRY(c, dmalloc(&c->d_smp, A * p2pmg::kDqnBatch * p2pmg::kTrans));
+  HIP_TRY(c, dmalloc(&c->d_smp, A * p2pmg::kDqnBatch));
   HIP_TRY(c, hipMemsetAsync(c->d_added, 0, A * 4, c->stream));
   HIP_TRY(c, dmalloc(&c->d_ep_acc, (size_t)c->S));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
