@@ -320,13 +320,15 @@ def main():
 
     def episode(e):
         if shared:
-            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record)
+            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record,
+                            next_epsilon=epsilon_at(e + 1))
             if world > 1:
                 eng.allreduce_q_delta()
             eng.apply_q_delta()
             eng.reset_temperatures_philox(e + 1, 0.3)  # agent.reset() at the end of train_episode
         else:  # the same reset, fused into the episode launch
-            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record, reset_sigma=0.3)
+            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record, reset_sigma=0.3,
+                            next_epsilon=epsilon_at(e + 1))
 
     for e in range(args.warmup):
         episode(e)

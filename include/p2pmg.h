@@ -127,6 +127,9 @@ typedef struct p2pmg_episode_args {
   int32_t flags;    /* P2PMG_FLAG_* (0 = automatic choice) */
   int32_t scen_per_wave; /* fast kernel: scenarios per 64-lane wave (0 = automatic: 64 / pow2ceil(N)) */
   double reset_sigma;    /* with P2PMG_FLAG_RESET_T0: sigma of the T0 draw */
+  double next_epsilon;   /* TRAIN + Philox, fast kernel: epsilon of the NEXT episode, for the
+                            speculative pre-pass this launch writes (<= 0: same as epsilon).
+                            A wrong guess only costs a pre-pass launch next time, never results. */
 } p2pmg_episode_args;
 
 /* Philox placement: a parallel pre-pass writing per-step code words (latency-bound batches:

@@ -65,7 +65,7 @@ class DqnConfig(C.Structure):
 class EpisodeArgs(C.Structure):
     _fields_ = [("mode", C.c_int32), ("rng", C.c_int32), ("episode", C.c_int32), ("record", C.c_int32),
                 ("epsilon", C.c_double), ("flags", C.c_int32), ("scen_per_wave", C.c_int32),
-                ("reset_sigma", C.c_double)]
+                ("reset_sigma", C.c_double), ("next_epsilon", C.c_double)]
 
 
 FLAG_PHILOX_PREPASS, FLAG_PHILOX_INKERNEL, FLAG_GENERAL_KERNEL, FLAG_RESET_T0 = 1, 2, 4, 8

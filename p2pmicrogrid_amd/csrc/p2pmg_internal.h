@@ -115,6 +115,7 @@ struct PrepOut {
   uint32_t* ipc;   // [T][A] or null (N != 2)
   uint32_t* words; // [T][W][A] or null (no Philox draws)
   int episode;
+  double eps;      // the epsilon its Philox draws are for
 };
 hipError_t launch_step_prepass(const EpisodeParams& p, const PrepOut& o, hipStream_t stream);
 // next != null: the launch also runs the step pre-pass of the next episode (episode p.episode + 1,

@@ -898,6 +898,7 @@ __device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOu
   if (o.words) {
     EpisodeParams q = p;
     q.episode = o.episode;
+    q.eps = o.eps;
     const int R1 = p.R + 1, W = (R1 + 3) >> 2;
     for (int w = 0; w < W; ++w) {
       uint32_t word = 0xFFFFFFFFu;
@@ -1440,7 +1441,7 @@ hipError_t launch_fast_n(const EpisodeParams& p, const uint2* pre, void* recs, i
   const int blocks = (p.S + spw - 1) / spw;
   const size_t n = (size_t)p.T * p.A;
   const int prod = nxt ? (int)std::min<size_t>(2048, (n + kWave - 1) / kWave) : 0;
-  const PrepOut none{nullptr, nullptr, nullptr, 0};
+  const PrepOut none{nullptr, nullptr, nullptr, 0, 0.0};
   FastRec* r = reinterpret_cast<FastRec*>(recs);
   switch (p.R + 1) {
     case 1: launch_fast_r<N, QT, 1>(p, pre, r, blocks, spw, prod, nxt ? *nxt : none, ev0, ev1, st); break;

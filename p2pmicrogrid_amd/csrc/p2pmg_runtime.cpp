@@ -662,18 +662,21 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     const bool hit = c->spec_valid[ps] && c->spec_version[ps] == c->inputs_version &&
                      (!philox || (c->spec_episode[ps] == args->episode && c->spec_eps[ps] == args->epsilon));
     if (!hit) {
-      const p2pmg::PrepOut o{c->pre[ps], p.pre_ipc, philox ? c->pcodes[ps] : nullptr, args->episode};
+      const p2pmg::PrepOut o{c->pre[ps], p.pre_ipc, philox ? c->pcodes[ps] : nullptr, args->episode,
+                             args->epsilon};
       HIP_TRY(c, p2pmg::launch_step_prepass(p, o, c->stream));
     }
-    // the next slot, for episode + 1 at the same epsilon (Philox draws only when this one has them)
+    // the next slot, for episode + 1 at the caller's next epsilon (the decay schedule is known,
+    // community.py:279-286; <= 0: the same epsilon).  Philox draws only when this one has them.
     const int ns = ps ^ 1;
+    const double next_eps = args->next_epsilon > 0.0 ? args->next_epsilon : args->epsilon;
     next = p2pmg::PrepOut{c->pre[ns], want_ipc ? c->pre_ipc[ns] : nullptr, philox ? c->pcodes[ns] : nullptr,
-                          args->episode + 1};
+                          args->episode + 1, next_eps};
     produce = true;
     c->spec_valid[ns] = true;
     c->spec_version[ns] = c->inputs_version;
     c->spec_episode[ns] = philox ? args->episode + 1 : -1;
-    c->spec_eps[ns] = args->epsilon;
+    c->spec_eps[ns] = next_eps;
   } else if (train && args->rng == P2PMG_RNG_PHILOX) {
     bool prepass = c->A < (1 << 18) && !sq16;  // sq16: throughput-bound, draws in the kernel
     if (args->flags & P2PMG_FLAG_PHILOX_PREPASS) prepass = true;

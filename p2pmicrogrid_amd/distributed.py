@@ -149,10 +149,13 @@ class ShardedTrainer:
             self.eng.set_q_delta(all_reduce_int64(self.eng.get_q_delta(), self.world))
         self.eng.apply_q_delta()
 
-    def train_episode(self, epsilon: float, reset_sigma: float = 0.3) -> float:
+    def train_episode(self, epsilon: float, reset_sigma: float = 0.3,
+                      next_epsilon: Optional[float] = None) -> float:
         """One training episode on every shard; returns the global mean over scenarios of the
-        episode reward (sum_t mean_i r, community.py:179)."""
-        self.eng.run_episode("train", "philox", episode=self.episode, epsilon=epsilon)
+        episode reward (sum_t mean_i r, community.py:179).  next_epsilon: the next episode's
+        epsilon (the decay schedule, community.py:279-286), for the speculative pre-pass."""
+        self.eng.run_episode("train", "philox", episode=self.episode, epsilon=epsilon,
+                             next_epsilon=next_epsilon)
         if self.shared_q:
             self.exchange_q_delta()
         local = self.eng.episode_reward().astype(np.float64)

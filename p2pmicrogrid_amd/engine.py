@@ -214,13 +214,17 @@ class DeviceCommunityBatch:
     # ----------------------------------------------------------------- the hot path
     def run_episode(self, mode: str = "train", rng: str = "replay", episode: int = 0, epsilon: float = 0.81,
                     record: Sequence[str] = (), philox: str = "auto", kernel: str = "auto",
-                    scen_per_wave: int = 0, reset_sigma: Optional[float] = None):
+                    scen_per_wave: int = 0, reset_sigma: Optional[float] = None,
+                    next_epsilon: Optional[float] = None):
         """Launch one episode for all scenarios (asynchronous; stream-ordered).
         philox: 'auto' | 'prepass' | 'inkernel' placement of the Philox draws.
         kernel: 'auto' (the fast per-agent-table kernel whenever it applies) | 'general'.
         scen_per_wave: fast kernel only, scenarios per 64-lane wave (0 = full waves).
         reset_sigma: end the episode with agent.reset() (community.py:181), i.e. exactly
-        reset_temperatures_philox(episode + 1, reset_sigma), fused into the episode launch."""
+        reset_temperatures_philox(episode + 1, reset_sigma), fused into the episode launch.
+        next_epsilon: the next episode's epsilon when the caller knows its decay schedule
+        (community.py:279-286), so that the speculative pre-pass this launch writes for
+        episode + 1 is a hit (None: the same epsilon)."""
         mask = 0
         for r in record:
             mask |= _lib.REC[r]
@@ -231,7 +235,7 @@ class DeviceCommunityBatch:
         args = _lib.EpisodeArgs(_lib.MODE_TRAIN if mode == "train" else _lib.MODE_GREEDY,
                                 _lib.RNG_REPLAY if rng == "replay" else _lib.RNG_PHILOX,
                                 int(episode), mask, float(epsilon), flags, int(scen_per_wave),
-                                float(reset_sigma or 0.0))
+                                float(reset_sigma or 0.0), float(next_epsilon or 0.0))
         self._chk(self.L.p2pmg_run_episode(self._ctx, C.byref(args)), "run_episode")
         self._recorded = mask
 

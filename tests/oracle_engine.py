@@ -42,7 +42,8 @@ class OracleEngine:
         a, b = philox.t0_draws(self.seed, episode, self.gids.ravel(), sigma=sigma)
         self.set_temperatures(a, b)
 
-    def run_episode(self, mode="train", rng="philox", episode=0, epsilon=0.81, record=(), philox="auto"):
+    def run_episode(self, mode="train", rng="philox", episode=0, epsilon=0.81, record=(), philox="auto",
+                    next_epsilon=None):  # next_epsilon: a device pre-pass hint, no effect on results
         self.last = self._ensure().run_episode(mode, rng="philox", seed=self.seed, episode=episode, eps=epsilon,
                                                agent_ids=self.gids)
 

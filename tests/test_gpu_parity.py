@@ -156,6 +156,23 @@ def test_philox_matches_oracle_and_t0(placement):
     assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
 
 
+def test_speculative_prepass_next_epsilon():
+    """next_epsilon: the launch writes episode e+1's Philox codes at the caller's next epsilon
+    (the decay schedule, community.py:279-286).  Right guesses (hits), wrong guesses (a recompute)
+    and no guess must all give the oracle's trajectory."""
+    S, N, R, T = 128, 2, 1, 48
+    inp = scenario_batch(S, N, T, seed=9)
+    ob = _oracle_for(inp, N, R)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = _device_for(inp, N, R)
+    eps = [0.81, 0.729, 0.729, 0.6561, 0.6561, 0.5]
+    guess = [0.729, 0.729, 0.3, None, 0.6561, None]  # hit, hit, miss, same-eps, hit, -
+    for e in range(len(eps)):
+        eng.run_episode("train", "philox", episode=e, epsilon=eps[e], record=REC, next_epsilon=guess[e])
+        _compare(ob.run_episode("train", rng="philox", seed=42, episode=e, eps=eps[e]), eng.get_records(REC), e)
+    assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
+
+
 def test_full_size_config2_sampled_against_oracle():
     """configs[1] at full size (4096 scenarios x thesis community): the whole batch runs on the
     device; 48 sampled scenarios are re-run by the oracle with the same global Philox ids, and
