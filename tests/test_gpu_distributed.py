@@ -26,7 +26,8 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     tr = ShardedTrainer(S_TOTAL, N, R, T, rank=rank, world=world, device=0)
-    means = [tr.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    # the ranks pass the schedule's next epsilon (speculative pre-pass hits), the single context not
+    means = [tr.train_episode(0.81 * 0.9 ** e, next_epsilon=0.81 * 0.9 ** (e + 1)) for e in range(EPISODES)]
     per = tr.episode_rewards_global()
     q_local = tr.eng.get_q(first=0, count=4)
     if rank == 0:
