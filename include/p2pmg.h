@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define P2PMG_ABI_VERSION 2
+#define P2PMG_ABI_VERSION 3  /* 3: p2pmg_episode_args.next_epsilon */
 
 typedef struct p2pmg_ctx p2pmg_ctx;
 

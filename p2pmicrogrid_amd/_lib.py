@@ -62,6 +62,9 @@ class DqnConfig(C.Structure):
                 ("capacity", C.c_int32), ("agents_per_block", C.c_int32), ("reserved", C.c_int32)]
 
 
+ABI_VERSION = 3  # include/p2pmg.h P2PMG_ABI_VERSION
+
+
 class EpisodeArgs(C.Structure):
     _fields_ = [("mode", C.c_int32), ("rng", C.c_int32), ("episode", C.c_int32), ("record", C.c_int32),
                 ("epsilon", C.c_double), ("flags", C.c_int32), ("scen_per_wave", C.c_int32),
@@ -165,7 +168,7 @@ def lib() -> C.CDLL:
             raise P2PMGError(f"libp2pmg.so not found at {path}; run `python -m p2pmicrogrid_amd._build`")
         _lib = C.CDLL(path)
         _declare(_lib)
-        if _lib.p2pmg_abi_version() != 2:
+        if _lib.p2pmg_abi_version() != ABI_VERSION:
             raise P2PMGError("libp2pmg ABI version mismatch")
         return _lib
 

@@ -24,7 +24,23 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_lib.EXPORTS)
-    assert L.p2pmg_abi_version() == 2
+    assert L.p2pmg_abi_version() == _lib.ABI_VERSION
+
+
+def _header_struct_fields(name):
+    txt = open(os.path.join(ROOT, "include", "p2pmg.h")).read()
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), txt, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    return [(t, f) for t, f in re.findall(r"(int32_t|double|float|int64_t|uint32_t)\s+(\w+)\s*;", body)]
+
+
+def test_episode_args_layout_matches_header():
+    """The ctypes mirror of p2pmg_episode_args has the header's fields, in order and type."""
+    import ctypes as C
+    from p2pmicrogrid_amd import _lib
+    ctype = {"int32_t": C.c_int32, "double": C.c_double}
+    hdr = _header_struct_fields("p2pmg_episode_args")
+    assert [(f, ctype[t]) for t, f in hdr] == list(_lib.EpisodeArgs._fields_)
 
 
 def test_config_default_matches_reference_constants():
