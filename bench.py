@@ -192,7 +192,7 @@ def main_dqn(args, rank, world, local, S, N, R, T):
             "config": {"workload": f"configs[4]: {S} scenarios/GPU x {N} DQN agents (R={R}, T={T}), one shared "
                                    f"5-64-64-1 Q-network, 32-sample batches per agent-step, Adam + soft update "
                                    f"per step, gradient all-reduce over ranks (RCCL)",
-                       "scenarios_per_gpu": S, "agents_per_scenario": N, "rounds": R + 1, "horizon": T,
+                       "scenarios_per_gpu": S, "agents_per_scenario": N, "rounds": R, "negotiation_rounds": R + 1, "horizon": T,
                        "agent_steps_per_step": world * steps_per_episode,
                        "parallelism": f"scenario-sharded x{world}, data-parallel shared network"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
@@ -385,7 +385,7 @@ def main():
             "dtype": "f32 simulation, f64 Q-table" if q_dtype == "f64" else "f32",
             "data": "synthetic profiles with the reference dataset schema (seed 42)",
             "config": {"workload": workload, "scenarios_per_gpu": S, "agents_per_scenario": N,
-                       "rounds": R + 1, "horizon": T, "q_dtype": q_dtype, "shared_q": shared, "battery": battery,
+                       "rounds": R, "negotiation_rounds": R + 1, "horizon": T, "q_dtype": q_dtype, "shared_q": shared, "battery": battery,
                        "agent_steps_per_step": world * steps_per_episode,
                        "parallelism": (f"scenario-sharded x{world}, shared-table delta all-reduce (RCCL)" if shared
                                        else f"scenario-sharded x{world} (replicas, no data-path collective)")},

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define P2PMG_ABI_VERSION 3  /* 3: p2pmg_episode_args.next_epsilon */
+#define P2PMG_ABI_VERSION 4  /* 3: p2pmg_episode_args.next_epsilon; 4: P2PMG_FLAG_NEXT_EPSILON, p2pmg_prepass_stats, per-network Adam steps */
 
 typedef struct p2pmg_ctx p2pmg_ctx;
 
@@ -128,8 +128,10 @@ typedef struct p2pmg_episode_args {
   int32_t scen_per_wave; /* fast kernel: scenarios per 64-lane wave (0 = automatic: 64 / pow2ceil(N)) */
   double reset_sigma;    /* with P2PMG_FLAG_RESET_T0: sigma of the T0 draw */
   double next_epsilon;   /* TRAIN + Philox, fast kernel: epsilon of the NEXT episode, for the
-                            speculative pre-pass this launch writes (<= 0: same as epsilon).
-                            A wrong guess only costs a pre-pass launch next time, never results. */
+                            speculative pre-pass this launch writes (see P2PMG_FLAG_NEXT_EPSILON;
+                            without the flag <= 0 means the same epsilon).  A wrong guess only
+                            costs a pre-pass launch next time, never results
+                            (p2pmg_prepass_stats counts hits and misses). */
 } p2pmg_episode_args;
 
 /* Philox placement: a parallel pre-pass writing per-step code words (latency-bound batches:
@@ -145,6 +147,9 @@ typedef struct p2pmg_episode_args {
  * drawn as p2pmg_reset_temperatures_philox(ctx, episode + 1, reset_sigma) would, fused into the
  * episode (no extra launch). */
 #define P2PMG_FLAG_RESET_T0 8
+/* next_epsilon holds the caller's guess as given, 0.0 included (DQN-style schedules decay to 0).
+ * Without this flag only a positive next_epsilon is a guess; anything else means "same epsilon". */
+#define P2PMG_FLAG_NEXT_EPSILON 16
 
 /* version / defaults */
 int p2pmg_abi_version(void);
@@ -178,7 +183,11 @@ int p2pmg_get_q(p2pmg_ctx* ctx, int first_agent, int count, void* host, int host
 
 /* the hot path */
 int p2pmg_run_episode(p2pmg_ctx* ctx, const p2pmg_episode_args* args);
-int p2pmg_get_record(p2pmg_ctx* ctx, int which, void* host);   /* one P2PMG_REC_* bit */
+/* one P2PMG_REC_* bit of the LAST episode launch; P2PMG_E_STATE if that launch did not record it */
+int p2pmg_get_record(p2pmg_ctx* ctx, int which, void* host);
+/* fast path: episode launches whose step pre-pass the previous launch had already produced (hits)
+ * and launches that had to run it themselves (misses), since the context was created */
+int p2pmg_prepass_stats(p2pmg_ctx* ctx, int64_t* hits, int64_t* misses);
 /* RuleAgent community run (get_rule_based_community community.py:237-238 -> run() community.py:95-123,
  * RuleAgent agent.py:106-136): hysteresis heat pump at the heat pump's max power (level 2 of
  * p2pmg_set_hp_levels), no policy, R = 0.  Records: COST, GRID, P2P, TEMP, ACTION (0 off / 2 on). */
@@ -270,8 +279,12 @@ int p2pmg_dqn_setup(p2pmg_ctx* ctx, const p2pmg_dqn_config* cfg);
 /* which = P2PMG_DQN_*; nets [first, first+count) of [count][P2PMG_DQN_PARAMS] f32 */
 int p2pmg_dqn_set_weights(p2pmg_ctx* ctx, int which, int first, int count, const float* host);
 int p2pmg_dqn_get_weights(p2pmg_ctx* ctx, int which, int first, int count, float* host);
-int p2pmg_dqn_set_step(p2pmg_ctx* ctx, int64_t step);   /* Adam iterations done (Keras `iterations`) */
+/* Adam iterations done (Keras `iterations`).  Each network has its own count (one optimizer per
+ * DQNAgent, agent.py:310): set_step sets every network's, get_step reads network 0's, an episode's
+ * env step advances every network's and p2pmg_dqn_train_batch only the network it trains. */
+int p2pmg_dqn_set_step(p2pmg_ctx* ctx, int64_t step);
 int p2pmg_dqn_get_step(p2pmg_ctx* ctx, int64_t* step);
+int p2pmg_dqn_get_net_steps(p2pmg_ctx* ctx, int first, int count, int64_t* steps);
 /* replay mode: deque indices (0 = oldest) of random.sample(buffer, 32) (rl.py:238) [T][A][32] */
 int p2pmg_dqn_set_samples(p2pmg_ctx* ctx, const uint16_t* samples);
 /* replay memory of agents [first, first+count): [count][capacity][10] f32 ring + added[count] */

@@ -37,16 +37,45 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=()) -> str:
-    """defines: extra -D flags (timing-only ablation builds go to a different ``out``)."""
+KERNEL_PARTS = 9  # p2pmg_kernels.hip is compiled once per part (-DP2PMG_PART=k), see its header
+
+
+def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=(), jobs: int = 0) -> str:
+    """defines: extra -D flags (timing-only ablation builds go to a different ``out``).
+    The translation units (9 parts of p2pmg_kernels.hip, p2pmg_dqn.hip, p2pmg_runtime.cpp) compile
+    in parallel into build/obj/<tag>/, then link into one shared library."""
     if out == LIB and not defines and not force and not needs_build():
         return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-Wno-pass-failed", f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
-           *[f"-D{d}" for d in defines], *[os.path.join(CSRC, s) for s in SOURCES], "-o", out + ".tmp"]
+    tag = "main" if not defines else "_".join(d.replace("=", "") for d in defines)
+    obj_dir = os.path.join(ROOT, "build", "obj", tag)
+    os.makedirs(obj_dir, exist_ok=True)
+    common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
+              "-Wall", "-Wno-unused-function", "-Wno-pass-failed", f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
+              *[f"-D{d}" for d in defines]]
+    units = [(os.path.join(CSRC, "p2pmg_kernels.hip"), [f"-DP2PMG_PART={k}"], f"kernels_{k}.o")
+             for k in range(KERNEL_PARTS)]
+    units += [(os.path.join(CSRC, s), [], os.path.splitext(s)[0] + ".o") for s in SOURCES if s != "p2pmg_kernels.hip"]
+    jobs = jobs or min(len(units), max(1, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    pending = list(units)
+    running = []
+    objs = []
+    while pending or running:
+        while pending and len(running) < jobs:
+            src, extra, o = pending.pop(0)
+            cmd = [*common, *extra, "-c", src, "-o", os.path.join(obj_dir, o)]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            running.append((subprocess.Popen(cmd), cmd))
+            objs.append(os.path.join(obj_dir, o))
+        proc, cmd = running.pop(0)
+        if proc.wait() != 0:
+            for q, _ in running:
+                q.wait()
+            raise subprocess.CalledProcessError(proc.returncode, cmd)
+    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+        print(" ".join(link), flush=True)
+    subprocess.run(link, check=True)
     os.replace(out + ".tmp", out)
     return out
 

@@ -37,7 +37,8 @@ EXPORTS = [
     "p2pmg_get_hp_state",
     "p2pmg_dqn_config_default", "p2pmg_dqn_setup", "p2pmg_dqn_set_weights", "p2pmg_dqn_get_weights",
     "p2pmg_dqn_set_step", "p2pmg_dqn_get_step", "p2pmg_dqn_set_samples", "p2pmg_dqn_get_buffer",
-    "p2pmg_dqn_set_buffer", "p2pmg_dqn_forward", "p2pmg_dqn_train_batch",
+    "p2pmg_dqn_set_buffer", "p2pmg_dqn_forward", "p2pmg_dqn_train_batch", "p2pmg_prepass_stats",
+    "p2pmg_dqn_get_net_steps",
 ]
 
 
@@ -62,7 +63,7 @@ class DqnConfig(C.Structure):
                 ("capacity", C.c_int32), ("agents_per_block", C.c_int32), ("reserved", C.c_int32)]
 
 
-ABI_VERSION = 3  # include/p2pmg.h P2PMG_ABI_VERSION
+ABI_VERSION = 4  # include/p2pmg.h P2PMG_ABI_VERSION
 
 
 class EpisodeArgs(C.Structure):
@@ -71,7 +72,7 @@ class EpisodeArgs(C.Structure):
                 ("reset_sigma", C.c_double), ("next_epsilon", C.c_double)]
 
 
-FLAG_PHILOX_PREPASS, FLAG_PHILOX_INKERNEL, FLAG_GENERAL_KERNEL, FLAG_RESET_T0 = 1, 2, 4, 8
+FLAG_PHILOX_PREPASS, FLAG_PHILOX_INKERNEL, FLAG_GENERAL_KERNEL, FLAG_RESET_T0, FLAG_NEXT_EPSILON = 1, 2, 4, 8, 16
 
 
 class P2PMGError(RuntimeError):
@@ -142,6 +143,8 @@ def _declare(lib):
         "p2pmg_dqn_set_buffer": ([vp, i32, i32, vp, vp], i32),
         "p2pmg_dqn_forward": ([vp, i32, i32, vp, vp], i32),
         "p2pmg_dqn_train_batch": ([vp, i32, vp, vp], i32),
+        "p2pmg_prepass_stats": ([vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)], i32),
+        "p2pmg_dqn_get_net_steps": ([vp, i32, i32, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -1,10 +1,15 @@
-"""Agents (mirrors microgrid/agent.py:23-298).
+"""Agents (mirrors microgrid/agent.py:23-350).
 
-Agents are parameter holders with the reference's constructors and attributes.  Their per-step
-methods (``__call__``, ``take_decision``, ``get_reward``, ``train``) are not called one agent at
-a time: ``CommunityMicrogrid`` fuses the whole negotiation / market / reward / TD / RC step of
-every agent into one device launch per episode (p2pmg_run_episode).  Calling them directly
-raises with a pointer to that path.
+Agents keep the reference's constructors and attributes.  Inside ``CommunityMicrogrid`` their
+per-step work is fused: one device launch per episode runs the negotiation, market, reward,
+TD update and RC step of every agent (p2pmg_run_episode).
+
+The per-agent step methods also exist, for callers that step agents themselves
+(``__call__``, ``take_decision``, ``get_reward``, ``train``, ``save_memory``, ``step``, ``reset``;
+agent.py:111-136, 200-250, 271-298, 312-342).  They run the reference's op order on f32 host
+values and call the device for the learner (QActor / Q-network calls, p2pmg_q_calls /
+p2pmg_dqn_*) and for the RC update (p2pmg_rc_step).  Each call is a handful of tiny launches:
+correct, but the batched community path is the one to use for throughput.
 """
 from __future__ import annotations
 
@@ -22,8 +27,37 @@ from . import rl
 from .rl import QActor
 from .storage import Storage
 
-_FUSED = ("per-agent step calls are fused into the community episode kernel; use "
-          "CommunityMicrogrid.train_episode() / run() (p2pmg_run_episode)")
+F32 = np.float32
+
+
+def _f32(x) -> np.ndarray:
+    return np.asarray(x.numpy() if hasattr(x, "numpy") else x, dtype=F32)
+
+
+def reduce_sum(v) -> np.float32:
+    """tf.math.reduce_sum of a small f32 vector in the build's canonical order, sequential from
+    +0.0 (the order the kernels and the oracle use)."""
+    acc = F32(0.0)
+    for x in _f32(v).ravel():
+        acc = F32(acc + x)
+    return acc
+
+
+def reduce_mean(v) -> np.float32:
+    v = _f32(v).ravel()
+    return F32(reduce_sum(v) / F32(v.size))
+
+
+def divide_power(out, powers) -> np.ndarray:
+    """RLAgent._divide_power (agent.py:186-195): keep the peers' powers of the opposite sign,
+    split ``out`` in proportion to them, or evenly over all N entries when none is kept."""
+    out = _f32(out).reshape(-1)
+    powers = _f32(powers).ravel()
+    filtered = np.where(np.sign(out) != np.sign(powers), powers, F32(0.0)).astype(F32)
+    total = np.abs(reduce_sum(filtered))
+    if total == F32(0.0):
+        return ((out * np.ones(powers.shape, F32)) / F32(powers.shape[0])).astype(F32)
+    return ((out * np.abs(filtered)) / total).astype(F32)
 
 
 class Agent(ABC):
@@ -78,9 +112,19 @@ class ActingAgent(Agent, ABC):
         self.max_in = max_in
         self.max_out = max_out  # stored, never read (community.py:228)
         self._load = load
+        self._load_pos = 0  # position of the reference's ``self.load`` generator (agent.py:79)
         self.pv = production
         self.storage = storage
         self.heating = heating
+
+    def _next_load_item(self):
+        """next(self.load): (x_t, x_{t+1}) of the load stream; StopIteration at its end."""
+        d = self._load
+        if self._load_pos >= len(d):
+            raise StopIteration
+        k = self._load_pos
+        self._load_pos += 1
+        return F32(np.asarray(d.data[k]).reshape(-1)[0]), F32(np.asarray(d.rolled[k]).reshape(-1)[0])
 
     @abstractmethod
     def __call__(self, *args, **kwargs): ...
@@ -96,6 +140,7 @@ class ActingAgent(Agent, ABC):
 
     def reset(self) -> None:
         super().reset()
+        self._load_pos = 0
         self.pv.reset()
         self.storage.reset()
         self.heating.reset()
@@ -114,46 +159,101 @@ class RuleAgent(ActingAgent):
     (``get_rule_based_community``) a whole run is one device launch (rule_episode_kernel)."""
 
     def __call__(self, *args, **kwargs):
-        raise NotImplementedError(_FUSED)
+        return self.take_decision(*args, **kwargs)
 
-    def take_decision(self, *args, **kwargs):
-        raise NotImplementedError(_FUSED)
+    def take_decision(self, *args, **kwargs) -> Tuple[np.ndarray, np.ndarray]:
+        """agent.py:116-128: hysteresis on the pre-step T_in, then (load - pv) + heat-pump power."""
+        t = F32(self.heating.temperature[0])
+        if t <= F32(self.heating.lower_bound):
+            self.heating.set_power(1)
+        elif t >= F32(self.heating.upper_bound):
+            self.heating.set_power(0)
+        current_load, _ = self._next_load_item()
+        current_pv, _ = self.pv.production
+        balance = F32(current_load - F32(current_pv))
+        return (np.array([balance], F32) + self.heating.power).astype(F32), np.array([0.], F32)
 
     def _update_storage(self, balance: float) -> float:
-        """agent.py:138-153: greedy battery rule on the net balance (W); returns the remainder.
-        The reference never calls it from a community; kept for scripts that do."""
-        energy = balance * setup.SECONDS_PER_MINUTE * setup.TIME_SLOT
-        if balance > 0 and self.storage.available_energy > 0:
-            to_extract = min(energy, self.storage.available_energy)
-            self.storage.discharge(self.storage.to_soc(to_extract))
-            balance -= to_extract / (setup.SECONDS_PER_MINUTE * setup.TIME_SLOT)
-        elif balance < 0 and not self.storage.is_full:
-            to_store = min(-energy, self.storage.available_space)
-            self.storage.charge(self.storage.to_soc(to_store))
-            balance += to_store / (setup.SECONDS_PER_MINUTE * setup.TIME_SLOT)
-        return balance
+        """agent.py:138-153 (never called by the reference's communities): the greedy battery
+        rule on one net balance (W), run on the device by the agent's storage (p2pmg_battery_seq)."""
+        return float(self.storage.apply_rule([balance])[0])
 
 
 class RLAgent(ActingAgent):
+    """agent.py:156-252.  The per-step methods run the reference's TF op order on f32 host
+    values; the learner calls (select/greedy action, TD update) run on the device."""
 
     def __init__(self, actor, *args, **kwargs):
         super().__init__(*args, **kwargs)
         self.actor = actor
+        self._next_load = self._next_load_item()        # agent.py:163-164
+        self._next_production = self.pv.production
+        self._current_balance = None
+        self._next_balance = None
+        self._current_state = None
+        self._action = None
+
+    def _get_balance(self) -> Tuple[np.ndarray, np.ndarray]:
+        """agent.py:172-176: (load - pv) / max_in of this step and of the next one."""
+        load, pv = self._next_load, self._next_production
+        mi = F32(self.max_in)
+        return (np.array([F32(load[0]) - F32(pv[0])], F32) / mi).astype(F32), \
+               (np.array([F32(load[1]) - F32(pv[1])], F32) / mi).astype(F32)
+
+    def _get_observation_state(self, state, balance, p2p) -> np.ndarray:
+        """agent.py:178-184: [time, normalised T_in, balance, p2p] as a (1, 4) f32 row."""
+        st = _f32(state)
+        time = st.reshape(-1)[:1] if st.ndim <= 1 else st[:, 0]
+        return np.concatenate([time, self.heating.normalized_temperature, _f32(balance).reshape(-1),
+                               _f32(p2p).reshape(1)]).astype(F32)[None, :]
+
+    def _divide_power(self, out, powers) -> np.ndarray:
+        return divide_power(out, powers)
+
+    def _act(self):
+        raise NotImplementedError
 
     def __call__(self, state, powers, *args, **kwargs):
-        raise NotImplementedError(_FUSED)
+        """agent.py:200-213: exploring decision for one negotiation round."""
+        powers = _f32(powers).ravel()
+        p2p = F32(reduce_mean(powers) / F32(self.max_in))
+        self._current_balance, self._next_balance = self._get_balance()
+        self._current_state = self._get_observation_state(state, self._current_balance, p2p)
+        q_val = self._act()
+        p_out = self._divide_power(self._current_balance * F32(self.max_in) + self.heating.power, powers)
+        return p_out, q_val
 
     def take_decision(self, state, powers, *args, **kwargs):
-        raise NotImplementedError(_FUSED)
+        raise NotImplementedError
 
-    def get_reward(self, cost):
-        raise NotImplementedError(_FUSED)
-
-    def train(self, reward, next_state, powers) -> float:
-        raise NotImplementedError(_FUSED)
+    def get_reward(self, cost) -> np.ndarray:
+        """agent.py:225-232: -(cost + 10 * penalty), penalty = distance outside the comfort band + 1."""
+        t = _f32(self.heating.temperature)
+        lo, hi = F32(self.heating.lower_bound), F32(self.heating.upper_bound)
+        pen = np.maximum(np.maximum(F32(0.0), lo - t), np.maximum(F32(0.0), t - hi)).astype(F32)
+        pen = np.where(pen > F32(0.0), pen + F32(1.0), F32(0.0)).astype(F32)
+        return (-(_f32(cost) + F32(10.0) * pen)).astype(F32)
 
     def save_memory(self, reward, next_state, powers) -> None:
-        raise NotImplementedError(_FUSED)
+        pass
+
+    def train(self, reward, next_state, powers) -> float:
+        raise NotImplementedError
+
+    def step(self) -> None:
+        """agent.py:234-241: advance the assets and the profile streams (None at their end)."""
+        super().step()
+        try:
+            self._next_load = self._next_load_item()
+            self._next_production = self.pv.production
+        except StopIteration:
+            self._next_load = None
+            self._next_production = None
+
+    def reset(self) -> None:
+        super().reset()
+        self._next_load = self._next_load_item()
+        self._next_production = self.pv.production
 
     def load_from_file(self, setting: str, implementation: str) -> None:
         self.actor.load_from_file(f'{re.sub("-", "_", setting)}_{self.id}', implementation)
@@ -177,6 +277,31 @@ class QAgent(RLAgent):
         self._actions = np.array([0., 0.5, 1.])
         self._last_action: int = -1
 
+    def _act(self):
+        """agent.py:271-275: epsilon-greedy on the device table, then the heat-pump set-point."""
+        self._last_action, q = self.actor.select_action(self._current_state)
+        self.heating.set_power(float(self._actions[self._last_action]))
+        return q
+
+    def take_decision(self, state, powers, *args, **kwargs):
+        """agent.py:277-289: greedy decision (evaluation)."""
+        powers = _f32(powers).ravel()
+        p2p = F32(reduce_mean(powers) / F32(self.max_in))
+        current_balance = self._get_balance()[0]
+        new_state = self._get_observation_state(state, current_balance, p2p)
+        action, q = self.actor.greedy_action(new_state)
+        self.heating.set_power(float(self._actions[action]))
+        p_out = self._divide_power(current_balance * F32(self.max_in) + self.heating.power, powers)
+        return p_out, q
+
+    def train(self, reward, next_state, powers) -> float:
+        """agent.py:293-298: TD update of the last round's (state, action) towards the next state
+        (p2p from ``powers``, the same pre-update T_in)."""
+        p2p = F32(reduce_mean(powers) / F32(self.max_in))
+        ns = self._get_observation_state(next_state, self._next_balance, p2p)
+        self.actor.train(self._current_state, self._last_action, reward, ns)
+        return 0.
+
 
 class DQNAgent(RLAgent):
     """Deep Q-learning agent (agent.py:301-350): ActorModel(epsilon=1), Trainer with a 5000-entry
@@ -187,6 +312,34 @@ class DQNAgent(RLAgent):
         super().__init__(rl.ActorModel(1), *args, **kwargs)
         self.trainer = rl.Trainer(self.actor, buffer_size=5 * 1000, batch_size=32, gamma=0.95, tau=0.005,
                                   optimizer=rl.Adam(learning_rate=1e-5))
+
+    def _act(self):
+        """agent.py:312-316"""
+        self._action, q_val = self.actor.select_action(self._current_state)
+        self.heating.set_power(float(self._action[0]))
+        return q_val
+
+    def take_decision(self, state, powers, *args, **kwargs):
+        """agent.py:318-331: greedy action of the Q-network (evaluation)."""
+        powers = _f32(powers).ravel()
+        p2p = F32(reduce_mean(powers) / F32(self.max_in))
+        current_balance = self._get_balance()[0]
+        new_state = self._get_observation_state(state, current_balance, p2p)
+        action, q = self.actor.greedy_action(new_state)
+        self.heating.set_power(float(action[0]))
+        p_out = self._divide_power(current_balance * F32(self.max_in) + self.heating.power, powers)
+        return p_out, q[:, 0]
+
+    def save_memory(self, reward, next_state, powers) -> None:
+        """agent.py:333-336: (s, a, r, s') into the agent's replay memory."""
+        p2p = F32(reduce_mean(powers) / F32(self.max_in))
+        ns = self._get_observation_state(next_state, self._next_balance, p2p)
+        self.trainer.buffer.add(self._current_state[0, :], self._action, _f32(reward), ns[0, :])
+
+    def train(self, reward, next_state, powers) -> float:
+        """agent.py:338-342"""
+        self.save_memory(reward, next_state, powers)
+        return self.trainer.train()
 
     def load_from_file(self, setting: str, implementation: str) -> None:
         super().load_from_file(setting, implementation)

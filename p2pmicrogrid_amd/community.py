@@ -26,7 +26,7 @@ from .environment import env
 from .heating import HeatPump, HPHeating
 from .production import PV, Prosumer
 from .rng import ReferenceRNG, dqn_episode_draws, python_random
-from .storage import NoStorage
+from .storage import BatteryStorage, NoStorage
 
 F32 = np.float32
 
@@ -113,6 +113,38 @@ class CommunityMicrogrid:
         t_in = np.array([a.heating.temperature[0] for a in self.agents], F32)
         t_m = np.array([a.heating.building_mass_temperature[0] for a in self.agents], F32)
         eng.set_temperatures(t_in[None], t_m[None])
+        self._push_storage(eng)
+
+    def _batteries(self) -> List[Optional[BatteryStorage]]:
+        return [a.storage if isinstance(a.storage, BatteryStorage) else None for a in self.agents]
+
+    def _push_storage(self, eng):
+        """Capacities and SoC of the agents' batteries (NoStorage = capacity 0) before a launch;
+        the kernels apply the battery rule (agent.py:138-153) to every round's net power."""
+        bats = self._batteries()
+        if not any(bats):
+            if self._uploaded.get("battery"):
+                eng.set_battery(None)
+                self._uploaded["battery"] = False
+            return
+        if self._dqn:
+            raise NotImplementedError("batteries are supported for tabular and rule-based communities")
+        ref = next(b for b in bats if b is not None).battery
+        for b in bats:
+            if b is not None and (b.battery.min_soc, b.battery.max_soc, b.battery.efficiency) != \
+                    (ref.min_soc, ref.max_soc, ref.efficiency):
+                raise ValueError("one community's batteries must share min_soc, max_soc and efficiency")
+        cap = np.array([0.0 if b is None else b.capacity for b in bats])[None]
+        soc = np.array([0.0 if b is None else b.soc for b in bats])[None]
+        eng.set_battery(cap, ref.min_soc, ref.max_soc, ref.efficiency, soc0=soc)
+        self._uploaded["battery"] = True
+
+    def _pull_storage(self, eng):
+        if self._uploaded.get("battery"):
+            soc = eng.get_soc()[0]
+            for b, x in zip(self._batteries(), soc):
+                if b is not None:
+                    b.set_soc(x)
 
     def _pull_records(self, eng, T):
         act = eng.get_record("action")[:, :, 0, :]  # [T, R+1, N]
@@ -136,6 +168,7 @@ class CommunityMicrogrid:
         codes = self._rng.episode_codes(T, self._rounds, N, eps)
         eng.set_replay_codes(codes)
         eng.run_episode("train", "replay", epsilon=float(eps[0]), record=("reward", "action"))
+        self._pull_storage(eng)
         self._pull_records(eng, T)
         self.last_rewards = eng.get_record("reward")[:, 0, :]
         avg_reward = float(eng.episode_reward()[0])
@@ -152,6 +185,7 @@ class CommunityMicrogrid:
         self._push_temperatures(eng)
         rec = ("grid", "p2p", "cost", "t_in", "action")
         eng.run_episode("greedy", record=rec)
+        self._pull_storage(eng)
         r = eng.get_records(rec)
         self._pull_records(eng, T)
         t_in, t_m = eng.get_temperatures()
@@ -228,6 +262,56 @@ class CommunityMicrogrid:
                 agent.reset()
         for agent in self.agents:
             agent.trainer.initialize_target()
+
+    # ------------------------------------------------------------ per-step API (host glue)
+    # For callers that step the community themselves, as community.py:149-182 does: the same
+    # TF op order on f32 host values (canonical sequential sums), with the agents'
+    # per-step methods calling the device for the learner and the RC update.
+    def _assign_powers(self, p2p_power) -> Tuple[np.ndarray, np.ndarray]:
+        """community.py:45-54: opposite-sign pairs exchange min(|P_ij|, |P_ji|), the rest is grid."""
+        P = np.asarray(p2p_power, F32)
+        p_match = np.where(np.sign(P) != np.sign(P.T), P, F32(0.0)).astype(F32)
+        exchange = (np.sign(p_match) * np.minimum(np.abs(p_match), np.abs(p_match).T)).astype(F32)
+        diff = (P - exchange).astype(F32)
+        p_grid = np.zeros(P.shape[0], F32)
+        p_p2p = np.zeros(P.shape[0], F32)
+        for j in range(P.shape[1]):
+            p_grid = (p_grid + diff[:, j]).astype(F32)
+            p_p2p = (p_p2p + exchange[:, j]).astype(F32)
+        return p_grid, p_p2p
+
+    def _compute_costs(self, grid_power, peer_power, buying_price, injection_price, p2p_price) -> np.ndarray:
+        """community.py:56-65 (prices [T] or scalars; powers [..., N])."""
+        g, pp = np.asarray(grid_power, F32), np.asarray(peer_power, F32)
+        buy = np.asarray(buying_price, F32).reshape(-1)[:, None]
+        inj = np.asarray(injection_price, F32).reshape(-1)[:, None]
+        p2p = np.asarray(p2p_price, F32).reshape(-1)[:, None]
+        c = (np.where(g >= F32(0.0), g * buy, g * inj) + pp * p2p).astype(F32)
+        return ((((c * F32(setup.TIME_SLOT)) / F32(setup.MINUTES_PER_HOUR)).astype(F32)) * F32(1e-3)).astype(F32)
+
+    def _run(self, time: int, state, training: bool = False):
+        """community.py:67-93: prices, R + 1 Jacobi negotiation rounds (each agent answers the
+        previous round's column, diagonal zeroed), market clearing on the final proposals."""
+        st = np.asarray(state.numpy() if hasattr(state, "numpy") else state, F32).reshape(-1)
+        buying_price, injection_price = self.grid.take_decision(st)
+        p2p_price = ((F32(buying_price) + np.asarray(injection_price, F32)) / F32(2)).astype(F32)
+        N = len(self.agents)
+        P = np.zeros((N, N), F32)
+        for r in range(self._rounds + 1):
+            P = (P - np.diag(np.diag(P))).astype(F32)
+            rows = []
+            for i, agent in enumerate(self.agents):
+                col = (-P[:, i]).astype(F32)
+                if training:
+                    action, _ = agent(st[None], col)
+                else:
+                    action, _ = agent.take_decision(st[None], col)
+                rows.append(np.asarray(action, F32).reshape(-1))
+            P = np.stack(rows).astype(F32)
+            for a, agent in enumerate(self.agents):
+                self.decisions[time, r, a] = float(agent.heating.power[0])
+        p_grid, p_p2p = self._assign_powers(P)
+        return p_grid, p_p2p, F32(buying_price), np.asarray(injection_price, F32), p2p_price
 
     def _step(self) -> None:
         for agent in self.agents:

@@ -235,12 +235,12 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
 
 // ----------------------------------------------------------------- train: Trainer._train
 __device__ __forceinline__ void adam_update(const DqnParams& d, float* th, float* tg, float* mm, float* vv, int idx,
-                                            float g) {
+                                            float g, float lr) {
   // Keras Adam (beta1 .9, beta2 .999, eps 1e-7) then Trainer._soft_update (rl.py:335-354)
   float m = mm[idx], v = vv[idx], w = th[idx];
   m = m + (g - m) * d.b1c;
   v = v + (g * g - v) * d.b2c;
-  w = w - (m * d.lr_t) / (sqrtf(v) + d.adam_eps);
+  w = w - (m * lr) / (sqrtf(v) + d.adam_eps);
   mm[idx] = m;
   vv[idx] = v;
   th[idx] = w;
@@ -524,21 +524,23 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     float* tg = d.target + (size_t)net_out * kNetStride;
     float* mm = d.adam_m + (size_t)net_out * kNetStride;
     float* vv = d.adam_v + (size_t)net_out * kNetStride;
+    // each DQNAgent has its own Adam (agent.py:310): its own iteration count, so its own step size
+    const float lr = d.lr_net ? d.lr_net[net_out] : d.lr_t;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) adam_update(d, th, tg, mm, vv, kOffW2 + (16 * mt + 4 * g4 + r) * kH + col, gW2[mt][r]);
+      for (int r = 0; r < 4; ++r) adam_update(d, th, tg, mm, vv, kOffW2 + (16 * mt + 4 * g4 + r) * kH + col, gW2[mt][r], lr);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int k = 4 * g4 + r;
-      if (k < 5) adam_update(d, th, tg, mm, vv, kOffW1 + k * kH + col, fminf(fmaxf(gW1[r], -d.clip), d.clip));
+      if (k < 5) adam_update(d, th, tg, mm, vv, kOffW1 + k * kH + col, fminf(fmaxf(gW1[r], -d.clip), d.clip), lr);
     }
     if (g4 == 0) {
-      adam_update(d, th, tg, mm, vv, kOffB1 + col, gb1);
-      adam_update(d, th, tg, mm, vv, kOffB2 + col, gb2);
-      adam_update(d, th, tg, mm, vv, kOffW3 + col, gW3);
+      adam_update(d, th, tg, mm, vv, kOffB1 + col, gb1, lr);
+      adam_update(d, th, tg, mm, vv, kOffB2 + col, gb2, lr);
+      adam_update(d, th, tg, mm, vv, kOffW3 + col, gW3, lr);
     }
-    if (threadIdx.x == 0) adam_update(d, th, tg, mm, vv, kOffB3, gb3);
+    if (threadIdx.x == 0) adam_update(d, th, tg, mm, vv, kOffB3, gb3, lr);
   } else {
     float* gp = d.grad + (size_t)blockIdx.x * kNetStride;
 #pragma unroll
@@ -602,7 +604,7 @@ __global__ void dqn_adam_shared_kernel(const DqnParams d) {
   if (k >= kDqnParams) return;
   float g = d.gsum[k] * d.inv_agents;
   if (k < kOffB1) g = fminf(fmaxf(g, -d.clip), d.clip);
-  adam_update(d, d.theta, d.target, d.adam_m, d.adam_v, k, g);
+  adam_update(d, d.theta, d.target, d.adam_m, d.adam_v, k, g, d.lr_t);
 }
 
 // QNetwork.call on explicit rows (object API, rl.py:147-148): one thread per row

@@ -89,6 +89,7 @@ struct DqnParams {
   float* rec_loss;           // [T][A] or null
   float* ep_acc;             // [S] running sum_t mean_i r
   float gamma, tau, tau_c, lr_t, b1c, b2c, adam_eps, clip;
+  const float* lr_net;       // per-agent networks whose Adam step counts differ: [n_nets] step sizes (else null: lr_t)
   float inv_agents;          // shared: 1 / (agents over all ranks)
   int apb;                   // agents per train workgroup
   const float* batch;        // explicit [32][kTrans] batch (p2pmg_dqn_train_batch) or null
@@ -123,6 +124,17 @@ hipError_t launch_step_prepass(const EpisodeParams& p, const PrepOut& o, hipStre
 // ev0 / ev1: timing events stamped by the dispatch (hipExtLaunchKernel)
 hipError_t launch_episode_fast(const EpisodeParams& p, const uint2* pre, void* recs, int q_dtype, int spw,
                                const PrepOut* next, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
+// the per-part launchers behind launch_episode_fast / launch_episode (p2pmg_kernels.hip, P2PMG_PART)
+#define P2PMG_DECL_FAST_PART(k)                                                                               \
+  hipError_t launch_fast_part##k(const EpisodeParams& p, const uint2* pre, void* recs, int q_dtype, int spw, \
+                                 const PrepOut* next, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
+P2PMG_DECL_FAST_PART(1)
+P2PMG_DECL_FAST_PART(2)
+P2PMG_DECL_FAST_PART(3)
+P2PMG_DECL_FAST_PART(4)
+hipError_t launch_general_part6(const EpisodeParams& p, int q_dtype, hipStream_t stream);
+hipError_t launch_general_part7(const EpisodeParams& p, int q_dtype, hipStream_t stream);
+hipError_t launch_general_part8(const EpisodeParams& p, int q_dtype, hipStream_t stream);
 // RuleAgent community run (R = 0): rule_episode_kernel; hp_on [A] hysteresis state in/out
 hipError_t launch_rule_episode(const EpisodeParams& p, float* hp_on, hipStream_t stream);
 // shared table, N = 16, R <= 1 (configs[2]): episode_sq16_kernel; records packed like the fast path

@@ -20,6 +20,16 @@
 
 #include "p2pmg_internal.h"
 
+// The file is compiled once per part (-DP2PMG_PART=k, in parallel by _build.py); each part defines
+// a disjoint subset of the launchers below, so each template kernel is instantiated in one part only.
+//   0: small kernels + dispatchers   1-4: episode_fast_kernel, N = 1-2 / 3-4 / 5-6 / 7-8
+//   5: episode_sq16_kernel           6-8: episode_kernel, N = 1-4 / 5-8 / 16
+// Without -DP2PMG_PART everything is in one translation unit.
+#ifndef P2PMG_PART
+#define P2PMG_PART -1
+#endif
+#define P2PMG_IN_PART(k) (P2PMG_PART < 0 || P2PMG_PART == (k))
+
 namespace p2pmg {
 namespace {
 
@@ -720,6 +730,7 @@ __global__ void apply_delta_kernel(QT* __restrict__ q, long long* __restrict__ d
 }
 
 // sum the per-XCD delta replicas into copy 0 (and clear the others)
+#if P2PMG_IN_PART(0)
 __global__ void fold_delta_kernel(long long* __restrict__ d, size_t n) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
@@ -734,8 +745,10 @@ __global__ void fold_delta_kernel(long long* __restrict__ d, size_t n) {
   }
   d[k] = x;
 }
+#endif
 
 // battery rule over per-agent sequences (unit parity with storage.py / agent.py:138-153)
+#if P2PMG_IN_PART(0)
 __global__ void battery_seq_kernel(int agents, int steps, const double* bal, double* out_bal, double* soc_hist,
                                    double* soc, const double* cap, double smin, double smax, double sqrt_eff) {
   const int a = blockIdx.x * blockDim.x + threadIdx.x;
@@ -748,9 +761,11 @@ __global__ void battery_seq_kernel(int agents, int steps, const double* bal, dou
   }
   soc[a] = s_;
 }
+#endif
 
 // Philox pre-pass: every (t, agent) code word of an episode in one parallel launch, so the
 // latency-bound episode loop only loads a prefetched word instead of computing R+1 blocks.
+#if P2PMG_IN_PART(0)
 __global__ void philox_codes_kernel(const EpisodeParams p, uint32_t* __restrict__ words) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
   if (k >= (size_t)p.T * p.A) return;
@@ -766,8 +781,10 @@ __global__ void philox_codes_kernel(const EpisodeParams p, uint32_t* __restrict_
     words[((size_t)t * W + w) * p.A + a] = word;
   }
 }
+#endif
 
 // host replay codes u8 [T][R1][A] -> code words [T][W][A]
+#if P2PMG_IN_PART(0)
 __global__ void pack_codes_kernel(int T, int R1, int A, const uint8_t* __restrict__ in, uint32_t* __restrict__ words) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (size_t)T * A) return;
@@ -782,6 +799,7 @@ __global__ void pack_codes_kernel(int T, int R1, int A, const uint8_t* __restric
     words[((size_t)t * W + w) * A + a] = word;
   }
 }
+#endif
 
 // ----------------------------------------------------------------- the fast per-agent-table path
 // IEEE f32 division a / b without its range handling.  hipcc's correctly rounded sequence is
@@ -911,11 +929,13 @@ __device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOu
     }
   }
 }
+#if P2PMG_IN_PART(0)
 __global__ void step_prepass_kernel(const EpisodeParams p, const PrepOut o) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
   if (k >= (size_t)p.T * p.A) return;
   prepass_one(p, o, k);
 }
+#endif
 
 // round 1 after an all-even round 0: every lane's row is ev (agent.py:190-191), so the column is
 // the group's ev values (one shuffle per partner instead of a row exchange)
@@ -1042,7 +1062,7 @@ struct FastRec {         // [T][A], 32 B
   uint32_t bins;         // (it * nT*nb + ib) | iT << 16
   uint32_t ips;          // byte r: p2p bin of round r
 };
-template <int N, typename QT, int R1, bool TRAIN, bool BAT>
+template <int N, typename QT, int R1, bool TRAIN, bool BAT, bool NARROW>
 __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams p, const uint2* __restrict__ pre,
                                                              FastRec* __restrict__ recs, int spw, int n_cons,
                                                              const PrepOut nxt) {
@@ -1093,9 +1113,12 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, np);  // round 0 and next state: p2p = 0 (agent.py:203)
   // stores of inactive lanes (and every record when none is requested) go to a per-lane dummy slot
   QT* const q_dummy = reinterpret_cast<QT*>(p.dummy) + lane * kQPad;
-  // records: FastRec rows, or only {reward, cost} as float2 when nothing else was requested
-  // (not in the battery variant: its loop measured 2 % slower with the extra branch)
-  const bool narrow = !BAT && p.rec_narrow != 0;
+  // records: FastRec rows, or only {reward, cost} as float2 when nothing else was requested.
+  // A compile-time choice: with a run-time branch between the two store sequences the compiler's
+  // vmcnt bookkeeping takes the shortest path through the branch, and the mid-step wait for the
+  // round-1 rows then also waits for the previous step's TD store to complete (an HBM write ack).
+  constexpr bool narrow = NARROW;
+  static_assert(!(BAT && NARROW), "the battery variant writes FastRec rows");
   const size_t rec_bytes = narrow ? sizeof(float2) : sizeof(FastRec);
   char* const rec_dummy = reinterpret_cast<char*>(reinterpret_cast<FastRec*>(p.dummy) + kWave + lane);
   const bool rec_on = p.record != 0 && active;
@@ -1114,17 +1137,23 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const uint2* preb = pre + a;
   const uint32_t* codes_a = p.codes + a;
   const uint32_t* ipc_a = p.pre_ipc + a;  // read only when CAND
-  const int t1 = T > 1 ? 1 : 0;
-  // running (uniform, 32-bit) offsets of step t + 2, wrapping at T: T * A < 2^32 on this path
+  const int t1 = T > 1 ? 1 : 0, t2 = 2 % T;
+  // The per-step inputs (env row, pre-pass word, code word, round-1 bins) are streamed three steps
+  // ahead: loaded at step t for step t + 3.  They are fresh HBM lines every step, and with one
+  // step of distance the mid-step wait for step t + 1's words exposed part of their latency.
+  // Running (uniform, 32-bit) offsets of step t + 3, wrapping at T: T * A < 2^32 on this path.
   const uint32_t TA = (uint32_t)T * (uint32_t)A, env_st = (uint32_t)env_step, env_end = env_st * (uint32_t)T;
-  uint32_t o2 = (uint32_t)(2 % T) * (uint32_t)A, eo2 = (uint32_t)(2 % T) * env_st;
+  uint32_t o3 = (uint32_t)(3 % T) * (uint32_t)A, eo3 = (uint32_t)(3 % T) * env_st;
 
   EnvRow e0 = load_env(envb);
   EnvRow e1 = load_env(envb + (size_t)t1 * env_step);
+  EnvRow e2 = load_env(envb + (size_t)t2 * env_step);
   uint2 p0 = preb[0];
   uint2 p1 = preb[(size_t)t1 * A];
+  uint2 p2 = preb[(size_t)t2 * A];
   const uint32_t c0 = codes_a[0];
   uint32_t c1 = codes_a[(size_t)t1 * A];
+  uint32_t c2 = codes_a[(size_t)t2 * A];
   auto code_of = [&](uint32_t w) { return (TRAIN && active) ? w : 0xFFFFFFFFu; };
   uint32_t cw = code_of(c0);
   int iT = temp_bin(tin);
@@ -1140,11 +1169,12 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   uint32_t aN = TRAIN ? nrow : a0;
   Row4<QT> row0 = gather_row(q + a0 * kQPad);
   Row4<QT> rowN = gather_row(q + aN * kQPad);
-  uint32_t ipc0 = 0, ipc1 = 0;
+  uint32_t ipc0 = 0, ipc1 = 0, ipc2 = 0;
   Row4<QT> cand[3];
   if constexpr (CAND) {
     ipc0 = ipc_a[0];
     ipc1 = ipc_a[(size_t)t1 * A];
+    ipc2 = ipc_a[(size_t)t2 * A];
 #pragma unroll
     for (int b = 0; b < 3; ++b) cand[b] = gather_row(q + (strip + ((ipc0 >> (8 * b)) & 0xFFu)) * kQPad);
   }
@@ -1207,14 +1237,14 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     const float ev0 = div_n_r<N>(out0 * 1.0f, rn);
 #pragma unroll
     for (int j = 0; j < N; ++j) row[j] = ev0;
-    EnvRow e2;
-    uint2 p2;
-    uint32_t c2, ipc2 = 0;
-    if constexpr (CAND) {  // no round-1 gather to hide behind: issue the step t + 2 inputs now
-      e2 = load_env(envb + eo2);
-      p2 = preb[o2];
-      c2 = codes_a[o2];
-      ipc2 = ipc_a[o2];
+    EnvRow e3;
+    uint2 p3;
+    uint32_t c3, ipc3 = 0;
+    if constexpr (CAND) {  // no round-1 gather to hide behind: issue the step t + 3 inputs now
+      e3 = load_env(envb + eo3);
+      p3 = preb[o3];
+      c3 = codes_a[o3];
+      ipc3 = ipc_a[o3];
     }
 #pragma unroll
     for (int r = 1; r < R1; ++r) {
@@ -1242,9 +1272,9 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
 #endif
       }
       if (!CAND && r == R1 - 1) {  // next inputs, issued behind the dependent gather
-        e2 = load_env(envb + eo2);
-        p2 = preb[o2];
-        c2 = codes_a[o2];
+        e3 = load_env(envb + eo3);
+        p3 = preb[o3];
+        c3 = codes_a[o3];
       }
       act = code == 255 ? argmax3(rowR) : code;
       acts |= (uint32_t)act << (8 * r);
@@ -1290,9 +1320,9 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       for (int j = 0; j < N; ++j) row[j] = (tot == 0.0f) ? ev : row[j];
     }
     if constexpr (R1 == 1) {
-      e2 = load_env(envb + eo2);
-      p2 = preb[o2];
-      c2 = codes_a[o2];
+      e3 = load_env(envb + eo3);
+      p3 = preb[o3];
+      c3 = codes_a[o3];
     }
     soc = soc_r;  // BatteryStorage state after the final round's decision
     pat.row = 0xFFFFFFFFu;  // the next step's rows were issued after the previous TD store
@@ -1330,11 +1360,11 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       *(active ? q + srow * kQPad + act : q_dummy) = qnew;
       pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
     }
-    if (narrow) {  // wave-uniform
-      *reinterpret_cast<float2*>(rec_ptr) = make_float2(rw, cost);
+    if constexpr (narrow) {
+      *reinterpret_cast<float2*>(__builtin_assume_aligned(rec_ptr, 8)) = make_float2(rw, cost);
     } else {
       const uint32_t bins = (p0.y & 0xFFFFu) | ((uint32_t)iT << 16);  // it * nT*nb + ib | iT << 16
-      float4* rp = reinterpret_cast<float4*>(rec_ptr);
+      float4* rp = reinterpret_cast<float4*>(__builtin_assume_aligned(rec_ptr, 16));
       rp[0] = make_float4(rw, cost, g, pp);
       rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
     }
@@ -1348,13 +1378,16 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     iT = iT1;
     e0 = e1;
     e1 = e2;
+    e2 = e3;
     p0 = p1;
     p1 = p2;
+    p2 = p3;
     c1 = c2;
-    o2 += (uint32_t)A;
-    o2 = o2 == TA ? 0u : o2;
-    eo2 += env_st;
-    eo2 = eo2 == env_end ? 0u : eo2;
+    c2 = c3;
+    o3 += (uint32_t)A;
+    o3 = o3 == TA ? 0u : o3;
+    eo3 += env_st;
+    eo3 = eo3 == env_end ? 0u : eo3;
     strip = strip1;
     cw = cw1;
     a0 = a0n;
@@ -1364,6 +1397,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     if constexpr (CAND) {
       ipc0 = ipc1;
       ipc1 = ipc2;
+      ipc2 = ipc3;
 #pragma unroll
       for (int b = 0; b < 3; ++b) cand[b] = candn[b];
     }
@@ -1386,6 +1420,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
 
 // FastRec rows -> the general record buffers (reward, cost, grid, p2p, tin [T][A]; action u8 and
 // packed index i32 [T][R+1][A]), for the records the caller asks for
+#if P2PMG_IN_PART(0)
 __global__ void fast_rec_unpack_kernel(int T, int R1, int A, uint32_t tb, const FastRec* __restrict__ recs, int narrow,
                                        int which, void* __restrict__ out) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
@@ -1411,18 +1446,27 @@ __global__ void fast_rec_unpack_kernel(int T, int R1, int A, uint32_t tb, const 
                                                       (((r.bins & 0xFFFFu) % tb) << 16) | (((r.ips >> (8 * rr)) & 0xFFu) << 24));
   }
 }
+#endif
 
 // hipExtLaunchKernel stamps the start / stop events from the dispatch itself: no marker packets
 // between back-to-back episodes
+template <int N, typename QT, int R1, bool BAT, bool NARROW>
+void launch_fast_nw(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
+                    const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  if (p.mode == 0)
+    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, true, BAT, NARROW>), dim3(blocks + prod), dim3(kWave), 0, st,
+                          ev0, ev1, 0, p, pre, recs, spw, blocks, nxt);
+  else
+    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, false, BAT, NARROW>), dim3(blocks + prod), dim3(kWave), 0, st,
+                          ev0, ev1, 0, p, pre, recs, spw, blocks, nxt);
+}
 template <int N, typename QT, int R1, bool BAT>
 void launch_fast_b(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
                    const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
-  if (p.mode == 0)
-    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, true, BAT>), dim3(blocks + prod), dim3(kWave), 0, st, ev0,
-                          ev1, 0, p, pre, recs, spw, blocks, nxt);
-  else
-    hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, false, BAT>), dim3(blocks + prod), dim3(kWave), 0, st, ev0,
-                          ev1, 0, p, pre, recs, spw, blocks, nxt);
+  if constexpr (!BAT) {
+    if (p.rec_narrow) return launch_fast_nw<N, QT, R1, false, true>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
+  }
+  launch_fast_nw<N, QT, R1, BAT, false>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
 }
 template <int N, typename QT, int R1>
 void launch_fast_r(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
@@ -1453,20 +1497,17 @@ hipError_t launch_fast_n(const EpisodeParams& p, const uint2* pre, void* recs, i
   return hipGetLastError();
 }
 
-template <typename QT>
-hipError_t launch_fast_q(const EpisodeParams& p, const uint2* pre, void* recs, int spw, const PrepOut* nxt,
-                         hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
-  switch (p.N) {
-    case 1: return launch_fast_n<1, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
-    case 2: return launch_fast_n<2, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
-    case 3: return launch_fast_n<3, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
-    case 4: return launch_fast_n<4, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
-    case 5: return launch_fast_n<5, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
-    case 6: return launch_fast_n<6, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
-    case 7: return launch_fast_n<7, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
-    case 8: return launch_fast_n<8, QT>(p, pre, recs, spw, nxt, ev0, ev1, st);
-    default: return hipErrorInvalidValue;
-  }
+// agents per scenario N0 and N0 + 1, f64 or f32 table
+template <int N0>
+hipError_t launch_fast_pair(const EpisodeParams& p, const uint2* pre, void* recs, int q_dtype, int spw,
+                            const PrepOut* nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  if (p.N == N0)
+    return q_dtype == 0 ? launch_fast_n<N0, double>(p, pre, recs, spw, nxt, ev0, ev1, st)
+                        : launch_fast_n<N0, float>(p, pre, recs, spw, nxt, ev0, ev1, st);
+  if (p.N == N0 + 1)
+    return q_dtype == 0 ? launch_fast_n<N0 + 1, double>(p, pre, recs, spw, nxt, ev0, ev1, st)
+                        : launch_fast_n<N0 + 1, float>(p, pre, recs, spw, nxt, ev0, ev1, st);
+  return hipErrorInvalidValue;
 }
 
 // ----------------------------------------------------------------- the fast shared-table path (N = 16)
@@ -1520,7 +1561,7 @@ __device__ __forceinline__ pkf2 fdiv_core_pk(pkf2 a, pkf2 b, pkf2 y) {
 #endif
 constexpr int kSq16Waves = 8;                        // waves per workgroup (one hash per 32 scenarios)
 constexpr int kTpStride = 16 * 16 + 16;              // floats per scenario tile (+16: bank offset)
-template <typename QT, int R1, bool TRAIN, bool BAT>
+template <typename QT, int R1, bool TRAIN, bool BAT, bool NARROW>
 __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq16_kernel(const EpisodeParams p) {
   constexpr int N = 16, G = 16, SPW = kWave / G;
   __shared__ uint32_t hkey[kSqSlots];
@@ -1586,8 +1627,9 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   uint32_t f1o = adv(0, A32, prof_end), f2o = adv(f1o, A32, prof_end);
   uint32_t c1o = (T > 1) ? code_step : 0;
   // records: FastRec rows, or only {reward, cost} as float2 when nothing else was requested
-  // (8 B instead of 32 B of writes per agent-step); masked-off lanes write a dummy row
-  const bool narrow = p.rec_narrow != 0;
+  // (8 B instead of 32 B of writes per agent-step); masked-off lanes write a dummy row.  Compile
+  // time, as in the fast kernel: no store-count branch for the vmcnt bookkeeping to be pessimistic about
+  constexpr bool narrow = NARROW;
   const size_t rec_bytes = narrow ? sizeof(float2) : sizeof(FastRec);
   char* const rec_dummy = reinterpret_cast<char*>(reinterpret_cast<FastRec*>(p.dummy) + kWave + lane);
   const bool rec_on = p.record != 0 && active;
@@ -1763,11 +1805,11 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
         lds_add_by_key(hkey, hval, (st.strip + (uint32_t)ip) * kQPad + (uint32_t)act, dv, dbase);
       }
     }
-    if (narrow) {
-      *reinterpret_cast<float2*>(rec_ptr) = make_float2(rw, cost);
+    if constexpr (narrow) {
+      *reinterpret_cast<float2*>(__builtin_assume_aligned(rec_ptr, 8)) = make_float2(rw, cost);
     } else {
       const uint32_t bins = (uint32_t)(st.it * D.T() * D.b() + st.ib) | ((uint32_t)st.iT << 16);
-      float4* rp = reinterpret_cast<float4*>(rec_ptr);
+      float4* rp = reinterpret_cast<float4*>(__builtin_assume_aligned(rec_ptr, 16));
       rp[0] = make_float4(rw, cost, g, pp);
       rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
     }
@@ -1816,16 +1858,21 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   }
 }
 
-template <typename QT, int R1>
-void launch_sq16_r(const EpisodeParams& p, int blocks, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+template <typename QT, int R1, bool NARROW>
+void launch_sq16_nw(const EpisodeParams& p, int blocks, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
   const dim3 g(blocks), b(kWave * kSq16Waves);
   if (p.mode == 0) {
-    if (p.battery) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, true>), g, b, 0, st, ev0, ev1, 0, p);
-    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, false>), g, b, 0, st, ev0, ev1, 0, p);
+    if (p.battery) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, true, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
+    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, false, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
   } else {
-    if (p.battery) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, true>), g, b, 0, st, ev0, ev1, 0, p);
-    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, false>), g, b, 0, st, ev0, ev1, 0, p);
+    if (p.battery) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, true, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
+    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, false, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
   }
+}
+template <typename QT, int R1>
+void launch_sq16_r(const EpisodeParams& p, int blocks, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  if (p.rec_narrow) launch_sq16_nw<QT, R1, true>(p, blocks, ev0, ev1, st);
+  else launch_sq16_nw<QT, R1, false>(p, blocks, ev0, ev1, st);
 }
 template <typename QT>
 hipError_t launch_sq16_q(const EpisodeParams& p, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
@@ -1933,23 +1980,13 @@ hipError_t launch_n(const EpisodeParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <typename QT>
-hipError_t launch_q(const EpisodeParams& p, hipStream_t st) {
-  switch (p.N) {
-    case 1: return launch_n<1, QT>(p, st);
-    case 2: return launch_n<2, QT>(p, st);
-    case 3: return launch_n<3, QT>(p, st);
-    case 4: return launch_n<4, QT>(p, st);
-    case 5: return launch_n<5, QT>(p, st);
-    case 6: return launch_n<6, QT>(p, st);
-    case 7: return launch_n<7, QT>(p, st);
-    case 8: return launch_n<8, QT>(p, st);
-    case 16: return launch_n<16, QT>(p, st);
-    default: return hipErrorInvalidValue;
-  }
+template <int N>
+hipError_t launch_nd(const EpisodeParams& p, int q_dtype, hipStream_t st) {
+  return q_dtype == 0 ? launch_n<N, double>(p, st) : launch_n<N, float>(p, st);
 }
 
 // ----------------------------------------------------------------- small kernels
+#if P2PMG_IN_PART(0)
 __global__ void rc_step_kernel(int n, const float* t_out, const float* t_in, const float* t_m, const float* hp,
                                float* t_in_new, float* t_m_new, RcParams rc) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1959,7 +1996,9 @@ __global__ void rc_step_kernel(int n, const float* t_out, const float* t_in, con
   t_in_new[k] = a;
   t_m_new[k] = b;
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 __global__ void state_indices_kernel(int n, const float* obs, int32_t* idx, int nt, int nT, int nb, int np) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
@@ -1969,13 +2008,16 @@ __global__ void state_indices_kernel(int n, const float* obs, int32_t* idx, int 
   idx[4 * k + 2] = idx_plain(o.z, nb);
   idx[4 * k + 3] = idx_plain(o.w, np);
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 __global__ void t0_philox_kernel(int A, float* t_in, float* t_m, uint32_t k0, uint32_t k1, int episode,
                                  uint32_t agent_offset, float setpoint, double sigma) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= A) return;
   t0_draw(k0, k1, episode, agent_offset + (uint32_t)k, setpoint, sigma, t_in[k], t_m[k]);
 }
+#endif
 
 // reference layout [count][n_states][n_actions] (host dtype) <-> padded device layout
 template <typename D, typename S>
@@ -1992,12 +2034,14 @@ __global__ void q_unpack_kernel(size_t rows, int na, const S* src, D* dst) {
   for (int c = 0; c < na; ++c) dst[k * na + c] = (D)src[k * kQPad + c];
 }
 
+#if P2PMG_IN_PART(0)
 __global__ void prof_pack_kernel(int A, int T, const float* load_w, const float* pv_w, float2* prof) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
   if (k >= (size_t)A * T) return;
   const int t = (int)(k / A), a = (int)(k % A);
   prof[k] = make_float2(load_w[(size_t)a * T + t], pv_w[(size_t)a * T + t]);
 }
+#endif
 
 // Standalone QActor calls, applied in order by a single thread (rl.py:89-129).
 template <typename QT>
@@ -2027,25 +2071,32 @@ inline unsigned grid_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1)
 
 }  // namespace
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_philox_codes(const EpisodeParams& p, uint32_t* words, hipStream_t stream) {
   const size_t n = (size_t)p.T * p.A;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(philox_codes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, p, words);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_pack_codes(int T, int R1, int A, const uint8_t* in, uint32_t* words, hipStream_t stream) {
   const size_t n = (size_t)T * A;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(pack_codes_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, T, R1, A, in, words);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_fold_delta(long long* qdelta, size_t n, hipStream_t stream) {
   hipLaunchKernelGGL(fold_delta_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, qdelta, n);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_apply_delta(void* q, long long* qdelta, size_t n, int q_dtype, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if (q_dtype == 0)
@@ -2054,7 +2105,9 @@ hipError_t launch_apply_delta(void* q, long long* qdelta, size_t n, int q_dtype,
     hipLaunchKernelGGL(apply_delta_kernel<float>, dim3(grid_for(n, 256)), dim3(256), 0, stream, (float*)q, qdelta, n);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_battery_seq(int agents, int steps, const double* bal, double* out_bal, double* soc_hist, double* soc,
                               const double* cap, double smin, double smax, double sqrt_eff, hipStream_t stream) {
   if (agents <= 0) return hipSuccess;
@@ -2062,20 +2115,45 @@ hipError_t launch_battery_seq(int agents, int steps, const double* bal, double* 
                      soc_hist, soc, cap, smin, smax, sqrt_eff);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_step_prepass(const EpisodeParams& p, const PrepOut& o, hipStream_t stream) {
   const size_t n = (size_t)p.T * p.A;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(step_prepass_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, p, o);
   return hipGetLastError();
 }
+#endif
 
+#define P2PMG_FAST_PART(k, N0)                                                                                   \
+  hipError_t launch_fast_part##k(const EpisodeParams& p, const uint2* pre, void* recs, int q_dtype, int spw,       \
+                                 const PrepOut* next, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream) {       \
+    return launch_fast_pair<N0>(p, pre, recs, q_dtype, spw, next, ev0, ev1, stream);                              \
+  }
+#if P2PMG_IN_PART(1)
+P2PMG_FAST_PART(1, 1)
+#endif
+#if P2PMG_IN_PART(2)
+P2PMG_FAST_PART(2, 3)
+#endif
+#if P2PMG_IN_PART(3)
+P2PMG_FAST_PART(3, 5)
+#endif
+#if P2PMG_IN_PART(4)
+P2PMG_FAST_PART(4, 7)
+#endif
+#if P2PMG_IN_PART(0)
 hipError_t launch_episode_fast(const EpisodeParams& p, const uint2* pre, void* recs, int q_dtype, int spw,
                                const PrepOut* next, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream) {
-  return q_dtype == 0 ? launch_fast_q<double>(p, pre, recs, spw, next, ev0, ev1, stream)
-                      : launch_fast_q<float>(p, pre, recs, spw, next, ev0, ev1, stream);
+  const int part = p.N <= 2 ? 1 : p.N <= 4 ? 2 : p.N <= 6 ? 3 : 4;
+  auto f = part == 1 ? launch_fast_part1 : part == 2 ? launch_fast_part2 : part == 3 ? launch_fast_part3 : launch_fast_part4;
+  if (p.N < 1 || p.N > 8) return hipErrorInvalidValue;
+  return f(p, pre, recs, q_dtype, spw, next, ev0, ev1, stream);
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void* recs, int narrow, int which, void* out,
                                   hipStream_t stream) {
   const size_t n = (size_t)T * A;
@@ -2084,11 +2162,15 @@ hipError_t launch_fast_rec_unpack(int T, int R1, int A, uint32_t tb, const void*
                      reinterpret_cast<const FastRec*>(recs), narrow, which, out);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(5)
 hipError_t launch_episode_sq16(const EpisodeParams& p, int q_dtype, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream) {
   return q_dtype == 0 ? launch_sq16_q<double>(p, ev0, ev1, stream) : launch_sq16_q<float>(p, ev0, ev1, stream);
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_rule_episode(const EpisodeParams& p, float* hp_on, hipStream_t stream) {
   const int n = p.N;
   if (n <= 1) launch_rule_g<1>(p, hp_on, stream);
@@ -2101,11 +2183,44 @@ hipError_t launch_rule_episode(const EpisodeParams& p, float* hp_on, hipStream_t
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
+#endif
 
-hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream) {
-  return q_dtype == 0 ? launch_q<double>(p, stream) : launch_q<float>(p, stream);
+#if P2PMG_IN_PART(6)
+hipError_t launch_general_part6(const EpisodeParams& p, int q_dtype, hipStream_t stream) {
+  switch (p.N) {
+    case 1: return launch_nd<1>(p, q_dtype, stream);
+    case 2: return launch_nd<2>(p, q_dtype, stream);
+    case 3: return launch_nd<3>(p, q_dtype, stream);
+    case 4: return launch_nd<4>(p, q_dtype, stream);
+    default: return hipErrorInvalidValue;
+  }
 }
+#endif
+#if P2PMG_IN_PART(7)
+hipError_t launch_general_part7(const EpisodeParams& p, int q_dtype, hipStream_t stream) {
+  switch (p.N) {
+    case 5: return launch_nd<5>(p, q_dtype, stream);
+    case 6: return launch_nd<6>(p, q_dtype, stream);
+    case 7: return launch_nd<7>(p, q_dtype, stream);
+    case 8: return launch_nd<8>(p, q_dtype, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+#endif
+#if P2PMG_IN_PART(8)
+hipError_t launch_general_part8(const EpisodeParams& p, int q_dtype, hipStream_t stream) {
+  return p.N == 16 ? launch_nd<16>(p, q_dtype, stream) : hipErrorInvalidValue;
+}
+#endif
+#if P2PMG_IN_PART(0)
+hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream) {
+  if (p.N >= 1 && p.N <= 4) return launch_general_part6(p, q_dtype, stream);
+  if (p.N >= 5 && p.N <= 8) return launch_general_part7(p, q_dtype, stream);
+  return launch_general_part8(p, q_dtype, stream);
+}
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_rc_step(int n, const float* t_out, const float* t_in, const float* t_m, const float* hp,
                           float* t_in_new, float* t_m_new, RcParams rc, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
@@ -2113,14 +2228,18 @@ hipError_t launch_rc_step(int n, const float* t_out, const float* t_in, const fl
                      t_m_new, rc);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_state_indices(int n, const float* obs, int32_t* idx, int nt, int nT, int nb, int np,
                                 hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(state_indices_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, obs, idx, nt, nT, nb, np);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_t0_philox(int A, float* t_in, float* t_m, uint32_t seed_lo, uint32_t seed_hi, int episode,
                             uint32_t agent_offset, float setpoint, double sigma, hipStream_t stream) {
   if (A <= 0) return hipSuccess;
@@ -2128,7 +2247,9 @@ hipError_t launch_t0_philox(int A, float* t_in, float* t_m, uint32_t seed_lo, ui
                      episode, agent_offset, setpoint, sigma);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_q_pack(int count, size_t n_states, int n_actions, const void* src_ref, void* dst_pad, int q_dtype,
                          int src_dtype, hipStream_t stream) {
   const size_t rows = (size_t)count * n_states;
@@ -2144,7 +2265,9 @@ hipError_t launch_q_pack(int count, size_t n_states, int n_actions, const void* 
     hipLaunchKernelGGL((q_pack_kernel<float, float>), g, b, 0, stream, rows, n_actions, (const float*)src_ref, (float*)dst_pad);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_q_unpack(int count, size_t n_states, int n_actions, const void* src_pad, void* dst_ref, int q_dtype,
                            int dst_dtype, hipStream_t stream) {
   const size_t rows = (size_t)count * n_states;
@@ -2160,7 +2283,9 @@ hipError_t launch_q_unpack(int count, size_t n_states, int n_actions, const void
     hipLaunchKernelGGL((q_unpack_kernel<float, float>), g, b, 0, stream, rows, n_actions, (const float*)src_pad, (float*)dst_ref);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_q_calls(const QCallParams& p, hipStream_t stream) {
   if (p.n <= 0) return hipSuccess;
   if (p.q_dtype == 0)
@@ -2169,12 +2294,15 @@ hipError_t launch_q_calls(const QCallParams& p, hipStream_t stream) {
     hipLaunchKernelGGL(q_calls_kernel<float>, dim3(1), dim3(64), 0, stream, p);
   return hipGetLastError();
 }
+#endif
 
+#if P2PMG_IN_PART(0)
 hipError_t launch_prof_pack(int A, int T, const float* load_w, const float* pv_w, float2* prof, hipStream_t stream) {
   const size_t n = (size_t)A * T;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(prof_pack_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, A, T, load_w, pv_w, prof);
   return hipGetLastError();
 }
+#endif
 
 }  // namespace p2pmg

@@ -59,6 +59,7 @@ struct p2pmg_ctx {
   double spec_eps[2] = {0.0, 0.0};
   long long spec_version[2] = {-1, -1};
   long long inputs_version = 0;  // bumped by every input upload (env, profiles, max_in, hp levels)
+  long long spec_hits = 0, spec_misses = 0;  // fast-path launches whose pre-pass was / was not ready
   bool mi_ok = false;         // every max_in inside the fast division range (fdiv in p2pmg_kernels.hip)
   void* dummy = nullptr;      // fast path: target of masked-off stores (2 * 64 * 32 B)
   void* rec_pack = nullptr;   // fast path: packed records [T][A] x 32 B
@@ -97,7 +98,10 @@ struct p2pmg_ctx {
   bool have_samples = false;
   float* d_ep_acc = nullptr;  // [S]
   float* rec_loss = nullptr;  // [T][A]
-  int64_t d_step = 0;
+  std::vector<int64_t> d_steps;  // Adam iterations done, per network (agent.py:310: one optimizer per agent)
+  float* d_lr = nullptr;      // [n_nets] per-network step sizes when the counts differ
+  std::vector<float> h_lr;
+  int rec_last_mask = 0;      // records the last episode launch wrote (p2pmg_get_record checks it)
   int64_t d_added_min = 0;    // every ring holds at least this many transitions
   std::string err;
   std::string last_kernel;
@@ -338,6 +342,7 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   dfree(c->d_target);
   dfree(c->d_m);
   dfree(c->d_v);
+  dfree(c->d_lr);
   dfree(c->d_grad);
   dfree(c->d_gsum);
   dfree(c->d_smp);
@@ -668,12 +673,19 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     }
     // the next slot, for episode + 1 at the caller's next epsilon (the decay schedule is known,
     // community.py:279-286; <= 0: the same epsilon).  Philox draws only when this one has them.
+    // P2PMG_NO_SPEC=1 (profiling only): no producer blocks, so the episode kernel's counters are its own
+    static const bool env_no_spec = [] { const char* v = getenv("P2PMG_NO_SPEC"); return v && atoi(v) != 0; }();
     const int ns = ps ^ 1;
-    const double next_eps = args->next_epsilon > 0.0 ? args->next_epsilon : args->epsilon;
+    // P2PMG_FLAG_NEXT_EPSILON: next_epsilon is the guess as given (0 included); without it a
+    // positive next_epsilon is the guess and anything else means "the same epsilon"
+    const bool have_next = (args->flags & P2PMG_FLAG_NEXT_EPSILON) != 0 || args->next_epsilon > 0.0;
+    const double next_eps = have_next ? args->next_epsilon : args->epsilon;
     next = p2pmg::PrepOut{c->pre[ns], want_ipc ? c->pre_ipc[ns] : nullptr, philox ? c->pcodes[ns] : nullptr,
                           args->episode + 1, next_eps};
-    produce = true;
-    c->spec_valid[ns] = true;
+    produce = !env_no_spec;
+    if (hit) c->spec_hits++;
+    else c->spec_misses++;
+    c->spec_valid[ns] = produce;
     c->spec_version[ns] = c->inputs_version;
     c->spec_episode[ns] = philox ? args->episode + 1 : -1;
     c->spec_eps[ns] = next_eps;
@@ -725,6 +737,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
                         : p2pmg::launch_episode(p, g.q_dtype, c->stream);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));
   c->rec_fast_mask = ext ? (args->record & 127) : 0;
+  c->rec_last_mask = args->record;
   c->rec_narrow = (fast || sq16) ? p.rec_narrow : 0;
   c->last_kernel = std::string(fast ? "episode_fast_kernel<" : sq16 ? "episode_sq16_kernel<" : "episode_kernel<") +
                    std::to_string(c->N) + "," + (g.q_dtype == 0 ? "f64" : "f32") + ",R1=" + std::to_string(c->R + 1) +
@@ -799,6 +812,7 @@ int p2pmg_run_rule_episode(p2pmg_ctx* c, int record) {
   HIP_TRY(c, p2pmg::launch_rule_episode(p, c->hp_on, c->stream));
   HIP_TRY(c, hipEventRecord(c->ring[2 * slot + 1], c->stream));
   c->rec_fast_mask = 0;
+  c->rec_last_mask = rec;
   c->last_kernel = "rule_episode_kernel<" + std::to_string(c->N) + ">";
   c->timed = true;
   c->n_timed++;
@@ -860,7 +874,8 @@ int p2pmg_get_record(p2pmg_ctx* c, int which, void* host) {
   } else {
     return fail(c, P2PMG_E_INVALID, "get_record: unknown record");
   }
-  if (!src) return fail(c, P2PMG_E_STATE, "get_record: record was never requested");
+  if (!src || !(c->rec_last_mask & which))
+    return fail(c, P2PMG_E_STATE, "get_record: the last episode launch did not record this");
   if (c->rec_fast_mask & which) {  // the last episode ran the fast kernel: unpack its rows
     const int w = slot >= 0 ? slot : (which == P2PMG_REC_ACTION ? 5 : 6);
     const uint32_t tb = (uint32_t)(c->cfg.n_temp_states * c->cfg.n_balance_states);
@@ -868,6 +883,13 @@ int p2pmg_get_record(p2pmg_ctx* c, int which, void* host) {
   }
   HIP_TRY(c, hipMemcpyAsync(host, src, bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_prepass_stats(p2pmg_ctx* c, int64_t* hits, int64_t* misses) {
+  if (!c) return P2PMG_E_INVALID;
+  if (hits) *hits = c->spec_hits;
+  if (misses) *misses = c->spec_misses;
   return P2PMG_OK;
 }
 
@@ -1169,7 +1191,9 @@ int p2pmg_dqn_setup(p2pmg_ctx* c, const p2pmg_dqn_config* cfg) {
   HIP_TRY(c, hipMemsetAsync(c->d_added, 0, A * 4, c->stream));
   HIP_TRY(c, dmalloc(&c->d_ep_acc, (size_t)c->S));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  c->d_step = 0;
+  c->d_steps.assign((size_t)c->n_nets, 0);
+  HIP_TRY(c, dmalloc(&c->d_lr, (size_t)c->n_nets));
+  c->h_lr.assign((size_t)c->n_nets, 0.0f);
   c->d_added_min = 0;
   return P2PMG_OK;
 }
@@ -1218,7 +1242,7 @@ int p2pmg_dqn_set_step(p2pmg_ctx* c, int64_t step) {
   int rc = dqn_ready(c, "dqn_set_step");
   if (rc != P2PMG_OK) return rc;
   if (step < 0) return P2PMG_E_INVALID;
-  c->d_step = step;
+  std::fill(c->d_steps.begin(), c->d_steps.end(), step);  // every network
   return P2PMG_OK;
 }
 
@@ -1226,7 +1250,15 @@ int p2pmg_dqn_get_step(p2pmg_ctx* c, int64_t* step) {
   int rc = dqn_ready(c, "dqn_get_step");
   if (rc != P2PMG_OK) return rc;
   if (!step) return P2PMG_E_INVALID;
-  *step = c->d_step;
+  *step = c->d_steps[0];
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_get_net_steps(p2pmg_ctx* c, int first, int count, int64_t* steps) {
+  int rc = dqn_ready(c, "dqn_get_net_steps");
+  if (rc != P2PMG_OK) return rc;
+  if (!steps || first < 0 || count < 0 || first + count > c->n_nets) return fail(c, P2PMG_E_INVALID, "dqn_get_net_steps");
+  for (int k = 0; k < count; ++k) steps[k] = c->d_steps[(size_t)first + k];
   return P2PMG_OK;
 }
 
@@ -1317,8 +1349,20 @@ static float adam_lr(const p2pmg_dqn_config& q, int64_t step) {
 }
 
 static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d) {
-  c->d_step++;
-  d.lr_t = adam_lr(c->dcfg, c->d_step);
+  // one env step trains every network once (community.py:158-168)
+  bool same = true;
+  for (auto& st : c->d_steps) {
+    ++st;
+    same = same && st == c->d_steps[0];
+  }
+  d.lr_t = adam_lr(c->dcfg, c->d_steps[0]);
+  d.lr_net = nullptr;
+  if (!same) {  // p2pmg_dqn_train_batch advanced some networks on their own: per-network step sizes
+    for (size_t k = 0; k < c->d_steps.size(); ++k) c->h_lr[k] = adam_lr(c->dcfg, c->d_steps[k]);
+    HIP_TRY(c, hipMemcpyAsync(c->d_lr, c->h_lr.data(), c->h_lr.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_lr is rewritten by the next step (rare path)
+    d.lr_net = c->d_lr;
+  }
   HIP_TRY(c, p2pmg::launch_dqn_sample(d, c->stream));
   if (c->n_nets == 1) {
     HIP_TRY(c, p2pmg::launch_dqn_train(d, c->d_blocks, true, c->stream));
@@ -1376,6 +1420,7 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   HIP_TRY(c, hipEventRecord(c->ring[2 * slot + 1], c->stream));
   c->timed = true;
   c->n_timed++;
+  c->rec_last_mask = args->record;
   if (acting) c->d_added_min += c->T;
   if (acting && args->rng == P2PMG_RNG_REPLAY) c->have_codes = c->code_src == 1;
   return P2PMG_OK;
@@ -1410,8 +1455,7 @@ int p2pmg_dqn_train_batch(p2pmg_ctx* c, int net, const float* batch, float* loss
   d.batch = db;
   d.net = net;
   d.loss_out = db + p2pmg::kDqnBatch * p2pmg::kTrans;
-  c->d_step++;
-  d.lr_t = adam_lr(c->dcfg, c->d_step);
+  d.lr_t = adam_lr(c->dcfg, ++c->d_steps[(size_t)net]);  // only this network's Adam iterates
   hipError_t e = hipMemcpyAsync(db, batch, (size_t)p2pmg::kDqnBatch * p2pmg::kTrans * 4, hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = p2pmg::launch_dqn_train(d, 1, false, c->stream);
   float l = 0.0f;

@@ -94,6 +94,13 @@ class DeviceDQNBatch(DeviceCommunityBatch):
     def step(self, value: int):
         self._chk(self.L.p2pmg_dqn_set_step(self._ctx, int(value)), "dqn_set_step")
 
+    def net_steps(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        """Adam iterations of each network (one optimizer per DQNAgent, agent.py:310)."""
+        count = self.n_nets - first if count is None else count
+        out = np.empty(count, np.int64)
+        self._chk(self.L.p2pmg_dqn_get_net_steps(self._ctx, first, count, out.ctypes.data), "dqn_get_net_steps")
+        return out
+
     # ----------------------------------------------------------------- replay memory
     def set_samples(self, samples):
         """Replay-mode sample indices: deque indices (0 = oldest) of random.sample(buffer, 32)

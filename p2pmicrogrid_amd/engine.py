@@ -232,6 +232,8 @@ class DeviceCommunityBatch:
         flags |= {"auto": 0, "general": _lib.FLAG_GENERAL_KERNEL}[kernel]
         if reset_sigma is not None:
             flags |= _lib.FLAG_RESET_T0
+        if next_epsilon is not None:  # a guess of 0.0 is a real guess (P2PMG_FLAG_NEXT_EPSILON)
+            flags |= _lib.FLAG_NEXT_EPSILON
         args = _lib.EpisodeArgs(_lib.MODE_TRAIN if mode == "train" else _lib.MODE_GREEDY,
                                 _lib.RNG_REPLAY if rng == "replay" else _lib.RNG_PHILOX,
                                 int(episode), mask, float(epsilon), flags, int(scen_per_wave),
@@ -257,6 +259,13 @@ class DeviceCommunityBatch:
         out = np.empty(self.A, F32)
         self._chk(self.L.p2pmg_get_hp_state(self._ctx, out), "get_hp_state")
         return out.reshape(self.S, self.N)
+
+    def prepass_stats(self):
+        """(hits, misses): fast-path launches whose step pre-pass the previous launch had produced
+        beside its own episode, and launches that had to run it themselves."""
+        h, m = C.c_int64(0), C.c_int64(0)
+        self._chk(self.L.p2pmg_prepass_stats(self._ctx, C.byref(h), C.byref(m)), "prepass_stats")
+        return int(h.value), int(m.value)
 
     def last_kernel(self) -> str:
         """Name of the kernel the last episode launch ran (fast or general path)."""

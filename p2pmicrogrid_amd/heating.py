@@ -167,6 +167,3 @@ class HPHeating(Heating):
     def get_history(self) -> List[float]:
         """heating.py:154-155: T_in before each step of the last run."""
         return self._history
-
-    def get_history(self) -> List[float]:
-        return self._history

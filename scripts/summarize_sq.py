@@ -1,0 +1,49 @@
+"""Per-launch averages of the SQ counter passes written by scripts/gpu_r02_sq.sh.
+
+For each workload, the episode kernel's counters (first launch dropped as warm-up) averaged over
+launches, plus derived figures: SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles
+(MI355X_MICROARCH.md constants table), so cycles = 4 x counter."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+out_dir = sys.argv[1]
+KERNEL = {"config2": "episode_fast_kernel", "config3": "episode_sq16_kernel"}
+res = {}
+for w, kname in KERNEL.items():
+    agg = collections.defaultdict(list)
+    for p in ("A", "B"):
+        files = glob.glob(os.path.join(out_dir, f"{w}_{p}", "**", "*counter_collection.csv"), recursive=True)
+        if not files:
+            continue
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        for r in csv.DictReader(open(files[0])):
+            if kname in r["Kernel_Name"]:
+                per[r["Counter_Name"]][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+        for c, d in per.items():
+            vals = [d[k] for k in sorted(d)]
+            vals = vals[1:] if len(vals) > 1 else vals
+            agg[c] = sum(vals) / len(vals)
+    if not agg:
+        continue
+    d = dict(agg)
+    waves = d.get("SQ_WAVES", 0) or 1
+    wc = d.get("SQ_WAVE_CYCLES", 0)
+    der = {
+        "wave_cycles_per_wave": 4 * wc / waves,
+        "frac_wait_any": d.get("SQ_WAIT_ANY", 0) / wc if wc else None,
+        "frac_wait_inst_any": d.get("SQ_WAIT_INST_ANY", 0) / wc if wc else None,
+        "frac_active_inst_any": d.get("SQ_ACTIVE_INST_ANY", 0) / wc if wc else None,
+        "valu_insts_per_wave": d.get("SQ_INSTS_VALU", 0) / waves,
+        "salu_insts_per_wave": d.get("SQ_INSTS_SALU", 0) / waves,
+        "vmem_rd_per_wave": d.get("SQ_INSTS_VMEM_RD", 0) / waves,
+        "vmem_wr_per_wave": d.get("SQ_INSTS_VMEM_WR", 0) / waves,
+        "lds_per_wave": d.get("SQ_INSTS_LDS", 0) / waves,
+        # one wave alone issues a VALU every 4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost')
+        "valu_issue_frac_of_one_wave_peak": (4 * d.get("SQ_INSTS_VALU", 0) / (4 * wc)) if wc else None,
+    }
+    res[w] = {"kernel": kname, "counters_per_launch": d, "derived": der}
+print(json.dumps(res, indent=1))

@@ -12,6 +12,8 @@ MagicMock that none of the functions below ever calls — SURVEY.md §8c):
   * ``rl.QActor._get_state_indices``       (rl.py:89-95)        -> qactor_idx.npz
   * ``rl.QActor.select_action/train/...``  (rl.py:100-132)      -> qactor_seq.npz, loop_*.npz
   * ``storage.BatteryStorage``             (storage.py:36-76)   -> battery.npz
+  * ``dataset.get_*_data``/``dataframe_to_dataset`` (dataset.py:39-103, database.py:128-147) on a
+    small SQLite file in the reference schema                -> dataset.npz
   * the legacy global ``np.random`` stream in the reference's consumption order (§3.5)
 
 The community glue that calls TF ops (agent.py:172-232, community.py:45-93,149-188) is
@@ -398,8 +400,80 @@ def make_battery(storage):
                         capacity=bat.capacity, min_soc=0.1, max_soc=0.9, efficiency=0.9, soc0=0.5)
 
 
+# ---------------------------------------------------------------- data pipeline (f2)
+DATASET_DAYS = (7, 8, 9, 11, 12, 13, 18, 19, 20, 21)  # 7 and 21 fall outside [start, end) (dataset.py:22-25)
+
+
+def dataset_raw(seed: int = 5):
+    """Raw rows of the two tables dataset.get_data reads (database.py:28-47 + the l0..l4 load
+    columns dataset.py:30 selects): a few October 2021 days; one load row is missing, so the
+    inner merge of database.get_data (database.py:145) drops that slot."""
+    rs = np.random.RandomState(seed)
+    env, load = [], []
+    for d in DATASET_DAYS:
+        for slot in range(96):
+            date, tm = f"2021-10-{d:02d}", f"{slot // 4:02d}:{15 * (slot % 4):02d}:00"
+            pv = max(0.0, float(np.sin(np.pi * (slot / 4.0 - 7.0) / 10.0))) * float(rs.uniform(200, 900))
+            env.append((date, tm, "+00:00", float(rs.normal(10, 3)), float(rs.rand()), float(rs.rand()), 0.0, pv))
+            if not (d == 12 and slot == 50):
+                load.append((date, tm, "+00:00", float(rs.uniform(100, 900)),
+                             *[float(rs.uniform(50, 2000)) for _ in range(5)]))
+    return env, load
+
+
+def write_dataset_db(path: str, env, load):
+    import sqlite3
+    con = sqlite3.connect(path)
+    cur = con.cursor()
+    cur.execute("CREATE TABLE environment (date text NOT NULL, time text NOT NULL, utc text NOT NULL, "
+                "temperature real, cloud_cover real, humidity real, irradiation real, pv real, "
+                "PRIMARY KEY (date, time, utc))")
+    cur.execute("CREATE TABLE load (date text NOT NULL, time text NOT NULL, utc text NOT NULL, load_0 real, "
+                "l0 real, l1 real, l2 real, l3 real, l4 real, PRIMARY KEY (date, time, utc))")
+    cur.executemany("INSERT INTO environment VALUES (?,?,?,?,?,?,?,?)", env)
+    cur.executemany("INSERT INTO load VALUES (?,?,?,?,?,?,?,?,?)", load)
+    con.commit()
+    con.close()
+
+
+def make_dataset():
+    """The reference's own dataset.get_train_data / get_validation_data / get_test_data
+    (dataset.py:61-95: database.get_data, day filter, process_dataframe) on a small database in
+    its schema, and the (x, np.roll(x, -1)) pair dataframe_to_dataset hands to tf.data
+    (dataset.py:98-103, captured from the TF mock)."""
+    import tempfile
+    env, load = dataset_raw()
+    tmp = tempfile.mkdtemp(prefix="p2pmg_golden_")
+    write_dataset_db(os.path.join(tmp, "ref.db"), env, load)
+    cfg = sys.modules["config"]
+    cfg.DB_FILE, cfg.DATA_PATH = "ref.db", tmp  # database.get_connection's defaults (database.py:16)
+    sys.modules.pop("database", None)
+    sys.modules.pop("dataset", None)
+    import dataset  # noqa: E402  (imports the reference's database with the config above)
+    out = {"env_rows": np.array([r[:3] for r in env]), "env_vals": np.array([r[3:] for r in env]),
+           "load_rows": np.array([r[:3] for r in load]), "load_vals": np.array([r[3:] for r in load])}
+    for split, fn in (("train", dataset.get_train_data), ("validation", dataset.get_validation_data),
+                      ("test", dataset.get_test_data)):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            env_df, agent_dfs = fn()
+        out[f"{split}_env_cols"] = np.array(list(env_df.columns))
+        out[f"{split}_env"] = env_df.to_numpy(dtype=np.float64)
+        out[f"{split}_index"] = env_df.index.to_numpy()
+        out[f"{split}_agents"] = np.stack([a.to_numpy(dtype=np.float64) for a in agent_dfs])
+        out[f"{split}_agent_cols"] = np.array(list(agent_dfs[0].columns))
+        if split == "train":
+            tfmock = sys.modules["tensorflow"]
+            tfmock.data.Dataset.from_tensor_slices.reset_mock()
+            dataset.dataframe_to_dataset(env_df)
+            x, xr = tfmock.data.Dataset.from_tensor_slices.call_args[0][0]
+            out["train_ds_x"], out["train_ds_rolled"] = np.asarray(x), np.asarray(xr)
+    np.savez_compressed(os.path.join(HERE, "dataset.npz"), **out)
+
+
 def main():
     heating, rl, storage, setup = import_reference()
+    make_dataset()
     assert setup.nr_agents == 2 and setup.rounds == 1 and setup.homogeneous is False
     make_heating(heating)
     make_qactor(rl)

@@ -73,6 +73,42 @@ def test_train_batch_matches_oracle_step():
     eng.close()
 
 
+def test_train_batch_keeps_one_adam_count_per_network():
+    """Each DQNAgent owns its Adam optimizer (agent.py:310), so training agent 0 then agent 1 of
+    one context gives BOTH networks bias-correction step 1, then 2 (not 1, 2, 3, 4); an episode
+    step afterwards advances each network's own count."""
+    eng = DeviceDQNBatch(1, 2, 1, 8, init_seed=4)
+    th = eng.get_weights("online")
+    tg = eng.get_weights("target")
+    rs = np.random.RandomState(5)
+    state = {n: (th[n:n + 1].copy(), tg[n:n + 1].copy(), np.zeros_like(th[n:n + 1]), np.zeros_like(th[n:n + 1]))
+             for n in (0, 1)}
+    for k in range(2):
+        for net in (0, 1):
+            s = rs.uniform(-1, 1, (32, 4)).astype(np.float32)
+            ns = rs.uniform(-1, 1, (32, 4)).astype(np.float32)
+            a = odqn.ACTION_VALUES[rs.randint(0, 3, 32)]
+            r = rs.uniform(-3, 0, 32).astype(np.float32)
+            eng.train_batch(s, a, r, ns, net=net)
+            th_o, tg_o, m, v = state[net]
+            g, _ = odqn.gradients(th_o, s[None], a[None], r[None], ns[None], tg_o, 0.95)
+            odqn.adam_step(th_o, m, v, g, k + 1)  # this network's own iteration count
+            odqn.soft_update(tg_o, th_o, 0.005)
+    assert list(eng.net_steps()) == [2, 2]
+    eng.train_batch(*[np.zeros(sh, np.float32) for sh in ((32, 4), 32, 32, (32, 4))], net=1)
+    assert list(eng.net_steps()) == [2, 3]
+    for net in (0, 1):
+        th_o, tg_o, m, v = state[net]
+        if net == 1:  # replay the extra zero batch on the oracle side too
+            z = np.zeros((1, 32, 4), np.float32)
+            g, _ = odqn.gradients(th_o, z, np.zeros((1, 32), np.float32), np.zeros((1, 32), np.float32), z, tg_o, 0.95)
+            odqn.adam_step(th_o, m, v, g, 3)
+            odqn.soft_update(tg_o, th_o, 0.005)
+        _rel_close(eng.get_weights("online")[net:net + 1] - th[net:net + 1], th_o - th[net:net + 1], rtol=2e-3)
+        _rel_close(eng.get_weights("adam_m")[net:net + 1], m, rtol=1e-4)
+    eng.close()
+
+
 def _pair(S, N, R, T, shared, init_seed=5):
     inp = scenario_batch(S, N, T)
     eng = DeviceDQNBatch(S, N, R, T, shared=shared, init_seed=init_seed)

@@ -165,11 +165,18 @@ def test_speculative_prepass_next_epsilon():
     ob = _oracle_for(inp, N, R)
     ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
     eng = _device_for(inp, N, R)
-    eps = [0.81, 0.729, 0.729, 0.6561, 0.6561, 0.5]
-    guess = [0.729, 0.729, 0.3, None, 0.6561, None]  # hit, hit, miss, same-eps, hit, -
+    eps = [0.81, 0.729, 0.729, 0.6561, 0.6561, 0.5, 0.0]
+    # guess[e] is launch e's guess of eps[e + 1]: right (launch e + 1 hits) or wrong (it misses);
+    # None = "the same epsilon"; 0.0 is a real guess (P2PMG_FLAG_NEXT_EPSILON), not "no guess"
+    guess = [0.729, 0.729, 0.3, None, 0.6561, 0.0, None]
+    expect_hit = [False, True, True, False, True, False, True]
     for e in range(len(eps)):
+        h0, _ = eng.prepass_stats()
         eng.run_episode("train", "philox", episode=e, epsilon=eps[e], record=REC, next_epsilon=guess[e])
+        h1, _ = eng.prepass_stats()
+        assert (h1 - h0 == 1) == expect_hit[e], f"launch {e}: pre-pass hit {h1 - h0 == 1}, expected {expect_hit[e]}"
         _compare(ob.run_episode("train", rng="philox", seed=42, episode=e, eps=eps[e]), eng.get_records(REC), e)
+    assert eng.prepass_stats() == (4, 3)
     assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
 
 
