@@ -1,0 +1,152 @@
+"""The bench workloads at their FULL per-GPU size (BASELINE.json configs[2] and configs[4]), on the
+kernels the bench runs, checked two ways: against another device path over EVERY scenario, and
+against the oracle on sampled scenarios (by global scenario id: the Philox counters and the
+scenario data depend only on the id, so a sampled subset is an independent problem).
+
+  configs[2]: 125,000 scenarios x 16 agents, battery, ONE shared f32 table (episode_sq16_kernel)
+              == the general episode_kernel on all 2M agents (records, int64 deltas, SoC, T),
+              32 sampled scenarios == oracle (the shared table is frozen per episode, so a
+              scenario's episode depends on the table and its own inputs only).
+  configs[4]: 4096 scenarios x 2 DQN agents.  Per-agent networks: 8 sampled scenarios == oracle
+              (actions and simulation exact, losses and weights within the f32 tolerance of
+              tests/test_gpu_dqn.py).  One shared network: whole-batch properties and bit-identical
+              results of two identical contexts (deterministic gradient reduction)."""
+import numpy as np
+import pytest
+
+from oracle import dqn as odqn
+from oracle.restatement import OracleBatch
+
+pytestmark = pytest.mark.gpu
+F32 = np.float32
+BATTERY_J = 10.0 * 3.6e6
+
+
+def _engine(inp, S, N, R, T, kernel_q, shared, battery):
+    from p2pmicrogrid_amd.engine import DeviceCommunityBatch
+    eng = DeviceCommunityBatch(S, N, R, T, q_dtype=kernel_q, shared_q=shared)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    if battery:
+        eng.set_battery(BATTERY_J)
+    return eng
+
+
+def test_full_size_config3_sq16_vs_general_and_sampled_oracle():
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    from p2pmicrogrid_amd.engine import unpack_index
+    S, N, R, T = 125000, 16, 1, 96
+    inp = scenario_batch(S, N, T)
+    a = _engine(inp, S, N, R, T, "f32", True, True)
+    b = _engine(inp, S, N, R, T, "f32", True, True)
+    pick = np.sort(np.random.RandomState(1).choice(S, 32, replace=False))
+    ob = OracleBatch(S=len(pick), N=N, R=R, load_w=inp.load_w[pick], pv_w=inp.pv_w[pick], max_in=inp.max_in[pick],
+                     env_time=inp.time[None], env_tout=inp.t_out[pick], q_dtype="f32", shared_q=True,
+                     battery_capacity=np.full((len(pick), N), BATTERY_J))
+    ob.t_in, ob.t_m = inp.t_in0[pick].copy(), inp.t_m0[pick].copy()
+    gids = pick[:, None] * N + np.arange(N)[None, :]
+    del inp
+    rec = ("reward", "cost", "t_in", "action", "index")
+    for e, eps in enumerate((0.81, 0.729)):
+        a.run_episode("train", "philox", episode=e, epsilon=eps, record=rec)
+        b.run_episode("train", "philox", episode=e, epsilon=eps, record=rec, kernel="general")
+        assert "sq16" in a.last_kernel() and "sq16" not in b.last_kernel()
+        for k in rec:  # every agent-step of both kernels
+            x, y = a.get_record(k), b.get_record(k)
+            assert np.array_equal(x, y), (e, k)
+            if k != "index":
+                del y
+        assert np.array_equal(a.get_q_delta(), b.get_q_delta()), e
+        assert np.array_equal(a.get_soc(), b.get_soc()), e
+        assert np.array_equal(a.episode_reward(), b.episode_reward()), e
+        for u, v in zip(a.get_temperatures(), b.get_temperatures()):
+            assert np.array_equal(u, v), e
+        # the sampled scenarios on the oracle, from the device's (frozen) table of this episode
+        out = ob.run_episode("train", rng="philox", seed=42, episode=e, eps=eps, agent_ids=gids)
+        rw, cost, tin = (a.get_record(k)[:, pick] for k in ("reward", "cost", "t_in"))
+        assert np.array_equal(rw, out["reward"]) and np.array_equal(cost, out["cost"]), e
+        assert np.array_equal(tin, out["t_in"]), e
+        assert np.array_equal(a.get_record("action")[:, :, pick], out["action"].astype(np.uint8)), e
+        assert np.array_equal(unpack_index(x[:, :, pick]), out["idx"]), e
+        assert np.array_equal(a.get_soc()[pick], ob.soc), e
+        a.apply_q_delta()
+        b.apply_q_delta()
+        qa = a.get_q(dtype=np.float32)
+        assert np.array_equal(qa, b.get_q(dtype=np.float32))
+        ob.q[0] = qa.reshape(ob.q[0].shape)  # the next episode reads the table all scenarios built
+        ob.q_delta[:] = 0
+    a.close()
+    b.close()
+
+
+def _dqn(inp, S, N, R, T, shared, init_seed=0):
+    from p2pmicrogrid_amd.dqn import DeviceDQNBatch
+    eng = DeviceDQNBatch(S, N, R, T, shared=shared, init_seed=init_seed)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    return eng
+
+
+def _rel_close(got, want, rtol, floor=1e-3):
+    want = np.asarray(want, np.float64)
+    scale = np.maximum(np.abs(want), floor * np.abs(want).max())
+    err = np.abs(np.asarray(got, np.float64) - want) / scale
+    assert err.max() <= rtol, f"max rel err {err.max():.3g}"
+
+
+def test_full_size_config5_dqn_per_agent_sampled_oracle():
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    S, N, R, T = 4096, 2, 1, 96
+    inp = scenario_batch(S, N, T)
+    eng = _dqn(inp, S, N, R, T, shared=False)
+    pick = np.sort(np.random.RandomState(2).choice(S, 8, replace=False))
+    agents = (pick[:, None] * N + np.arange(N)[None, :]).ravel()
+    th0 = eng.get_weights("online")
+    ob = odqn.OracleDQNBatch(S=len(pick), N=N, R=R, load_w=inp.load_w[pick], pv_w=inp.pv_w[pick],
+                             max_in=inp.max_in[pick], env_time=inp.time[None], env_tout=inp.t_out[pick],
+                             theta0=th0[agents], shared=False)
+    ob.t_in, ob.t_m = inp.t_in0[pick].copy(), inp.t_m0[pick].copy()
+    rec = ("reward", "cost", "grid", "p2p", "t_in", "action")
+    for e, (mode, eps) in enumerate((("fill", 1.0), ("train", 0.9))):
+        eng.run_episode(mode, "philox", episode=e, epsilon=eps, record=rec + (("loss",) if mode == "train" else ()))
+        out = ob.run_episode(mode, rng="philox", episode=e, eps=eps, agent_ids=agents)
+        got = eng.get_records(rec)
+        assert np.array_equal(got["action"][:, :, pick], out["action"].astype(np.uint8)), e
+        for k in ("reward", "cost", "grid", "p2p", "t_in"):
+            assert np.array_equal(got[k][:, pick], out[k]), (e, k)
+        if mode == "train":
+            _rel_close(eng.get_record("loss")[:, pick], out["loss"], rtol=1e-4)
+            # properties over every agent of the batch
+            assert np.all(np.isfinite(eng.get_record("loss")))
+        assert np.all(got["action"] <= 2) and np.all(got["p2p"].sum(axis=-1) == 0)
+    th = eng.get_weights("online")[agents]
+    _rel_close(th - th0[agents], ob.theta - th0[agents], rtol=1e-2, floor=1e-2)
+    eng.close()
+
+
+def test_full_size_config5_dqn_shared_network_properties():
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    S, N, R, T = 4096, 2, 1, 96
+    inp = scenario_batch(S, N, T)
+    a = _dqn(inp, S, N, R, T, shared=True)
+    b = _dqn(inp, S, N, R, T, shared=True)
+    w0 = a.get_weights("online")
+    for e, (mode, eps) in enumerate((("fill", 1.0), ("train", 0.9), ("train", 0.81))):
+        for x in (a, b):
+            x.run_episode(mode, "philox", episode=e, epsilon=eps, record=("reward", "p2p", "action"))
+            x.reset_temperatures_philox(e + 1, 0.3)
+        ra, rb = a.get_records(("reward", "p2p", "action")), b.get_records(("reward", "p2p", "action"))
+        for k in ra:
+            assert np.array_equal(ra[k], rb[k]), (e, k)  # deterministic reduction: same bits
+        assert np.all(np.isfinite(ra["reward"])) and np.all(ra["action"] <= 2)
+        assert np.all(ra["p2p"].sum(axis=-1) == 0)  # N = 2: the P2P exchange is antisymmetric
+    wa, wb = a.get_weights("online"), b.get_weights("online")
+    assert np.array_equal(wa, wb) and np.all(np.isfinite(wa))
+    assert not np.array_equal(wa, w0)  # 2 x 96 Adam steps moved the network
+    assert a.step == 2 * T
+    a.close()
+    b.close()
