@@ -210,6 +210,12 @@ int p2pmg_set_timing_period(p2pmg_ctx* ctx, int period);
 int p2pmg_rc_step(p2pmg_ctx* ctx, int n, const float* t_out, const float* t_in, const float* t_m,
                   const float* hp, float* t_in_new, float* t_m_new);
 int p2pmg_state_indices(p2pmg_ctx* ctx, int n, const float* obs /* [n][4] */, int32_t* idx /* [n][4] */);
+/* The kernels' fast divisions next to the IEEE operator, for the division fuzz test (the quotients
+ * the reference takes in agent.py:175,193,203, community.py:63 and storage.py:58,61,64).
+ * f32: out [n][4] = {fdiv_b, the divide-power form, the packed sq16 form, IEEE a / b};
+ * f64: out [n][3] = {fdiv64, qcore64 under the battery rule's guard, IEEE a / b}. */
+int p2pmg_fdiv_check(p2pmg_ctx* ctx, int n, const float* a, const float* b, float* out);
+int p2pmg_fdiv64_check(p2pmg_ctx* ctx, int n, const double* a, const double* b, double* out);
 
 /* heterogeneous agents and storage (configs 3-4) */
 int p2pmg_set_hp_levels(p2pmg_ctx* ctx, const float* levels /* [A][3] W per action */);

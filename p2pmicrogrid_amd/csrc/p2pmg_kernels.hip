@@ -1537,8 +1537,10 @@ __device__ __forceinline__ bool in_range19(float x) {
 }
 // fdiv_core on a packed pair with the residual negated, r' = b q - a: the same quotient bit for
 // bit (round-to-nearest is sign-symmetric, and an exact-zero residual is +0 either way, which
-// leaves q unchanged), and for a = +-0 it keeps sign(a) without fdiv_core's copysign:
-// q0 = +-0, r' = +0, q = fma(-0, y, +-0) = +-0.  Both lanes round like the scalar fma.
+// leaves q unchanged), and for a = +-0 with a POSITIVE divisor (the only use: tot = |sum| > 0) it
+// keeps sign(a) without fdiv_core's copysign: q0 = +-0, r' = +0, q = fma(-0, y, +-0) = +-0.  (With
+// a negative divisor q0 = -+0 and the last fma returns +0 for a = +0: not the IEEE -0; the division
+// fuzz test checks the positive-divisor domain.)  Both lanes round like the scalar fma.
 __device__ __forceinline__ pkf2 fdiv_core_pk(pkf2 a, pkf2 b, pkf2 y) {
   const pkf2 q0 = a * y;
   pkf2 r = __builtin_elementwise_fma(b, q0, -a);
@@ -2043,6 +2045,49 @@ __global__ void prof_pack_kernel(int A, int T, const float* load_w, const float*
 }
 #endif
 
+// The fast quotients of the episode kernels next to the IEEE operator, for the division fuzz test
+// (tests/test_gpu_division.py): exactly the guarded sequences the kernels run.
+//   f32 out[0] fdiv_b (hoisted reciprocal of a divisor checked on the host, IEEE when the numerator
+//              is out of range)            - max_in, 60, N, the comfort margin
+//       out[1] the divide-power form: recip of a data-dependent divisor, fdiv_core, IEEE when the
+//              divisor or the numerator is out of range
+//       out[2] the packed sq16 form (fdiv_core_pk) under its range-19 guard, else out[1]'s form
+//       out[3] IEEE a / b
+//   f64 out[0] fdiv64 (hoisted Recip64 + range test), out[1] qcore64 under q64_ok (battery_rule_r's
+//       guard), out[2] IEEE n / d
+#if P2PMG_IN_PART(0)
+__global__ void fdiv_check_kernel(int n, const float* __restrict__ a, const float* __restrict__ b,
+                                  float* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const float x = a[k], d = b[k];
+  const Recip r = recip(d);
+  out[4 * (size_t)k + 0] = r.ok ? fdiv_b(x, r) : fdiv_ieee(x, d);
+  float q1 = fdiv_core(x, r);
+  if (!r.ok || !fdiv_ok(x)) q1 = fdiv_ieee(x, d);
+  out[4 * (size_t)k + 1] = q1;
+  float q2 = q1;
+  if (r.ok && in_range19(x) && in_range19(d) && d > 0.0f) {  // the kernel's divisor is tot = |sum| > 0
+    const pkf2 y2 = {r.y, r.y}, b2 = {d, d};
+    q2 = fdiv_core_pk(pkf2{x, x}, b2, y2).x;
+  }
+  out[4 * (size_t)k + 2] = q2;
+  out[4 * (size_t)k + 3] = fdiv_ieee(x, d);
+}
+__global__ void fdiv64_check_kernel(int n, const double* __restrict__ a, const double* __restrict__ b,
+                                    double* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double x = a[k], d = b[k];
+  const Recip64 r = recip64(d);
+  out[3 * (size_t)k + 0] = fdiv64(x, r);
+  double q1 = qcore64(x, r);
+  if (!(r.ok && q64_ok(x))) q1 = fdiv64_ieee(x, d);
+  out[3 * (size_t)k + 1] = q1;
+  out[3 * (size_t)k + 2] = fdiv64_ieee(x, d);
+}
+#endif
+
 // Standalone QActor calls, applied in order by a single thread (rl.py:89-129).
 template <typename QT>
 __global__ void q_calls_kernel(const QCallParams p) {
@@ -2292,6 +2337,19 @@ hipError_t launch_q_calls(const QCallParams& p, hipStream_t stream) {
     hipLaunchKernelGGL(q_calls_kernel<double>, dim3(1), dim3(64), 0, stream, p);
   else
     hipLaunchKernelGGL(q_calls_kernel<float>, dim3(1), dim3(64), 0, stream, p);
+  return hipGetLastError();
+}
+#endif
+
+#if P2PMG_IN_PART(0)
+hipError_t launch_fdiv_check(int n, const float* a, const float* b, float* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fdiv_check_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, a, b, out);
+  return hipGetLastError();
+}
+hipError_t launch_fdiv64_check(int n, const double* a, const double* b, double* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fdiv64_check_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, a, b, out);
   return hipGetLastError();
 }
 #endif

@@ -925,6 +925,34 @@ int p2pmg_rc_step(p2pmg_ctx* c, int n, const float* t_out, const float* t_in, co
   return P2PMG_OK;
 }
 
+extern "C++" template <typename T, typename L>
+static int div_check(p2pmg_ctx* c, int n, const T* a, const T* b, T* out, int per, L launch, const char* what) {
+  if (!c || n < 0 || (n > 0 && (!a || !b || !out))) return P2PMG_E_INVALID;
+  if (n == 0) return P2PMG_OK;
+  T *da = nullptr, *db = nullptr, *dout = nullptr;
+  hipError_t e = dmalloc(&da, (size_t)n);
+  if (e == hipSuccess) e = dmalloc(&db, (size_t)n);
+  if (e == hipSuccess) e = dmalloc(&dout, (size_t)n * per);
+  if (e == hipSuccess) e = hipMemcpyAsync(da, a, (size_t)n * sizeof(T), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(db, b, (size_t)n * sizeof(T), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = launch(n, da, db, dout, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dout, (size_t)n * per * sizeof(T), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(da);
+  dfree(db);
+  dfree(dout);
+  if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return P2PMG_OK;
+}
+
+int p2pmg_fdiv_check(p2pmg_ctx* c, int n, const float* a, const float* b, float* out) {
+  return div_check(c, n, a, b, out, 4, p2pmg::launch_fdiv_check, "fdiv_check");
+}
+
+int p2pmg_fdiv64_check(p2pmg_ctx* c, int n, const double* a, const double* b, double* out) {
+  return div_check(c, n, a, b, out, 3, p2pmg::launch_fdiv64_check, "fdiv64_check");
+}
+
 int p2pmg_state_indices(p2pmg_ctx* c, int n, const float* obs, int32_t* idx) {
   if (!c || n < 0 || !obs || !idx) return P2PMG_E_INVALID;
   if (n == 0) return P2PMG_OK;

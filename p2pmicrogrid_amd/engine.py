@@ -322,6 +322,23 @@ class DeviceCommunityBatch:
         shape = np.broadcast(t_out, t_in, t_m, hp).shape
         return a.reshape(shape), b.reshape(shape)
 
+    def fdiv_check(self, a, b):
+        """The kernels' fast f32 quotients of a / b and the IEEE one: [n, 4] (p2pmg_fdiv_check)."""
+        a = np.ascontiguousarray(np.asarray(a, F32).ravel())
+        b = np.ascontiguousarray(np.asarray(b, F32).ravel())
+        out = np.empty((a.size, 4), F32)
+        self._chk(self.L.p2pmg_fdiv_check(self._ctx, a.size, a.ctypes.data, b.ctypes.data, out.ctypes.data), "fdiv_check")
+        return out
+
+    def fdiv64_check(self, a, b):
+        """The kernels' fast f64 quotients and the IEEE one: [n, 3] (p2pmg_fdiv64_check)."""
+        a = np.ascontiguousarray(np.asarray(a, np.float64).ravel())
+        b = np.ascontiguousarray(np.asarray(b, np.float64).ravel())
+        out = np.empty((a.size, 3), np.float64)
+        self._chk(self.L.p2pmg_fdiv64_check(self._ctx, a.size, a.ctypes.data, b.ctypes.data, out.ctypes.data),
+                  "fdiv64_check")
+        return out
+
     def state_indices(self, obs):
         """Batched QActor._get_state_indices (rl.py:89-95) on the device; obs [..., 4]."""
         o = np.ascontiguousarray(np.asarray(obs, dtype=F32).reshape(-1, 4))
