@@ -10,8 +10,12 @@ T0 reset (heating.py:145-152) + exploration draws + the fused episode kernel.  D
 synthetic profiles with the reference schema (the SQLite source is not available).
 
 N GPUs: one process per GPU (torchrun), scenarios sharded with no data-path collective (each
-scenario's tables are private: "replicas only"); torch.distributed(gloo) carries only the
-barrier and the max-over-ranks time.  value = all ranks' agent-steps / max time (weak scaling).
+scenario's tables are private: "replicas only").  Every workload creates an RCCL communicator
+over the ranks (xGMI); the episode metrics (sum and count of the episode rewards, community.py:179)
+are all-reduced over it every ``--metric-every`` episodes (the reference's logging cadence,
+community.py:279-288) and after the last one, and the line reports ``rccl_nranks`` as the
+communicator counts them.  torch.distributed(gloo) carries only the id broadcast, the barrier and
+the max-over-ranks time.  value = all ranks' agent-steps / max time (weak scaling).
 
 ``--workload config4`` (BASELINE.json configs[3]): 8192 scenarios x 4 households per GPU with
 heterogeneous asset mixes (dataset.asset_mix: Consumers without PV, no / 3 kW / 5 kW heat pumps,
@@ -81,6 +85,44 @@ def barrier(world):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+
+
+def rccl_comm(eng, rank: int, world: int, required: bool = False) -> str:
+    """The RCCL communicator of the rank's context (rank 0's unique id broadcast over gloo).
+    Returns "" or the error; a rank without a communicator reports its metrics over gloo, so a
+    replicas-only workload still runs (required=True: the shared-state workloads need it)."""
+    if world == 1:
+        return ""
+    from p2pmicrogrid_amd.distributed import broadcast_bytes
+    from p2pmicrogrid_amd.engine import comm_unique_id
+    uid = None
+    if rank == 0:
+        try:
+            uid = comm_unique_id()
+        except Exception:  # noqa: BLE001  (every rank learns it from the empty id)
+            uid = b""
+    uid = broadcast_bytes(uid, world)
+    if not uid:
+        if required:
+            raise RuntimeError("RCCL unavailable: the shared-state workloads need the device all-reduce")
+        return "no RCCL unique id"
+    try:
+        eng.comm_init(uid, rank, world)
+    except Exception as e:  # noqa: BLE001
+        if required:
+            raise
+        return f"{type(e).__name__}: {e}"
+    return ""
+
+
+def episode_metrics(eng, world: int, comm_err: str):
+    """(sum, count) of the episode rewards over every rank: RCCL, or gloo without a communicator."""
+    if not comm_err:
+        return eng.allreduce_metrics()
+    from p2pmicrogrid_amd.distributed import all_reduce_sum
+    local = eng.episode_reward().astype(np.float64)
+    tot = all_reduce_sum(np.array([local.sum(), local.size]), world)
+    return float(tot[0]), int(tot[1])
 
 
 def max_over_ranks(x: float, world: int) -> float:
@@ -154,10 +196,7 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     eng.set_max_in(inp.max_in)
     eng.set_temperatures(inp.t_in0, inp.t_m0)
     del inp
-    if world > 1:
-        from p2pmicrogrid_amd.distributed import broadcast_bytes
-        from p2pmicrogrid_amd.engine import comm_unique_id
-        eng.comm_init(broadcast_bytes(comm_unique_id() if rank == 0 else None, world), rank, world)
+    comm_err = rccl_comm(eng, rank, world, required=True)  # gradient all-reduce every env step + metrics
     record = ("reward", "cost")
     eng.run_episode("fill", "philox", episode=0, epsilon=1.0, record=record)  # community.init_buffers
     eng.reset_temperatures_philox(1, 0.3)
@@ -173,8 +212,11 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     barrier(world)
     eng.sync()
     t0 = time.perf_counter()
-    for e in range(1 + args.warmup, 1 + args.warmup + args.steps):
+    metrics = None
+    for k, e in enumerate(range(1 + args.warmup, 1 + args.warmup + args.steps)):
         episode(e)
+        if (k + 1) % args.metric_every == 0 or k + 1 == args.steps:
+            metrics = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
     eng.sync()
     barrier(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
@@ -200,7 +242,8 @@ def main_dqn(args, rank, world, local, S, N, R, T):
                          "kernel": "DQN episode: T x (dqn_act_kernel + dqn_train_kernel + reduce + adam)",
                          "kernel_ms": episode_ms, "flop_per_agent_step": flop,
                          "flop_per_episode": flop * steps_per_episode, "timed_launches": int(len(kms))},
-            "mean_episode_reward": float(np.mean(eng.episode_reward())),
+            "mean_episode_reward": metrics[0] / metrics[1],
+            "rccl_nranks": eng.comm_nranks() if not comm_err else 0,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_dqn(args.cpu_seconds, R=R, T=T)
@@ -277,6 +320,8 @@ def main():
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--q-dtype", default=None, choices=["f64", "f32"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--metric-every", type=int, default=50,
+                    help="episodes between RCCL all-reduces of the episode metrics (community.py:279)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary for roofline.traffic (default profiles/pmc_traffic[_<workload>].json)")
@@ -312,10 +357,8 @@ def main():
         eng.set_battery(mix.battery_capacity)
     elif battery:
         eng.set_battery(BATTERY_J)
-    if shared and world > 1:  # RCCL communicator for the per-episode delta all-reduce (xGMI)
-        from p2pmicrogrid_amd.distributed import broadcast_bytes
-        from p2pmicrogrid_amd.engine import comm_unique_id
-        eng.comm_init(broadcast_bytes(comm_unique_id() if rank == 0 else None, world), rank, world)
+    # episode metrics (+ the shared table's per-episode delta all-reduce, which needs RCCL)
+    comm_err = rccl_comm(eng, rank, world, required=shared)
     record = ("reward", "cost")
 
     def episode(e):
@@ -340,14 +383,19 @@ def main():
     barrier(world)
     eng.sync()
     t0 = time.perf_counter()
-    for e in range(args.warmup, args.warmup + args.steps):
+    metrics = None
+    for k, e in enumerate(range(args.warmup, args.warmup + args.steps)):
         episode(e)
+        if (k + 1) % args.metric_every == 0 or k + 1 == args.steps:
+            metrics = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
     eng.sync()
     barrier(world)
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dt, world)
     kms = eng.kernel_times()
-    ep_reward = float(np.mean(eng.episode_reward()))
+    ep_reward = metrics[0] / metrics[1]
+    nranks = eng.comm_nranks() if not comm_err else 0
+    hashes = eng.table_hash_allgather() if shared else None  # every replica of the shared table
 
     steps_per_episode = S * N * T
     value = world * steps_per_episode * args.steps / dt
@@ -398,7 +446,13 @@ def main():
                          "algorithmic_bytes_per_launch": bpa * steps_per_episode,
                          "timed_launches": int(len(kms)), "timing_period": timing_period},
             "mean_episode_reward": ep_reward,
+            "rccl_nranks": nranks,
         }
+        if comm_err:
+            out["rccl_error"] = comm_err
+        if shared:
+            out["table_replicas_identical"] = bool(np.all(hashes == hashes[0]))
+            assert out["table_replicas_identical"], f"shared-table replicas differ across ranks: {hashes}"
         if traffic:
             out["roofline"]["traffic_source"] = traffic.get("source")
         if world == 1 and not args.no_cpu_baseline:

@@ -238,6 +238,15 @@ int p2pmg_comm_unique_id(uint8_t id[128]);
 int p2pmg_comm_init(p2pmg_ctx* ctx, const uint8_t id[128], int rank, int nranks);
 int p2pmg_allreduce_q_delta(p2pmg_ctx* ctx);        /* int64 sum over ranks, in place, on the stream */
 int p2pmg_comm_destroy(p2pmg_ctx* ctx);
+/* ranks of the context's communicator (ncclCommCount; 1 without one) */
+int p2pmg_comm_nranks(p2pmg_ctx* ctx, int* nranks);
+/* episode metrics of the last episode over every rank: out = {sum over scenarios of the episode
+ * reward (community.py:179), number of scenarios}; the local sum in f64 on the device, then an
+ * RCCL all-reduce (sum) when a communicator exists.  Synchronises. */
+int p2pmg_allreduce_metrics(p2pmg_ctx* ctx, double* out /* [2] */);
+/* 64-bit fingerprint of the context's Q-table bits, all-gathered over the communicator:
+ * out[nranks] in rank order (out[0] alone without one); replicas of a shared table agree. */
+int p2pmg_table_hash_allgather(p2pmg_ctx* ctx, uint64_t* out);
 
 /* Standalone QActor calls (rl.py:89-129) on the context's per-agent tables, applied IN ORDER
  * by one device thread: for entry k, s = indices(s_obs[k]); a = codes[k] == P2PMG_GREEDY ?

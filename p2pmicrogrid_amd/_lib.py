@@ -38,7 +38,8 @@ EXPORTS = [
     "p2pmg_dqn_config_default", "p2pmg_dqn_setup", "p2pmg_dqn_set_weights", "p2pmg_dqn_get_weights",
     "p2pmg_dqn_set_step", "p2pmg_dqn_get_step", "p2pmg_dqn_set_samples", "p2pmg_dqn_get_buffer",
     "p2pmg_dqn_set_buffer", "p2pmg_dqn_forward", "p2pmg_dqn_train_batch", "p2pmg_prepass_stats",
-    "p2pmg_dqn_get_net_steps", "p2pmg_fdiv_check", "p2pmg_fdiv64_check",
+    "p2pmg_dqn_get_net_steps", "p2pmg_fdiv_check", "p2pmg_fdiv64_check", "p2pmg_comm_nranks",
+    "p2pmg_allreduce_metrics", "p2pmg_table_hash_allgather",
 ]
 
 
@@ -147,6 +148,9 @@ def _declare(lib):
         "p2pmg_dqn_get_net_steps": ([vp, i32, i32, vp], i32),
         "p2pmg_fdiv_check": ([vp, i32, vp, vp, vp], i32),
         "p2pmg_fdiv64_check": ([vp, i32, vp, vp, vp], i32),
+        "p2pmg_comm_nranks": ([vp, C.POINTER(C.c_int)], i32),
+        "p2pmg_allreduce_metrics": ([vp, vp], i32),
+        "p2pmg_table_hash_allgather": ([vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

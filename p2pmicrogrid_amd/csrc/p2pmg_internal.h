@@ -176,6 +176,8 @@ struct QCallParams {
   double alpha, gamma;
 };
 hipError_t launch_q_calls(const QCallParams& p, hipStream_t stream);
+hipError_t launch_metrics(int S, const float* ep, double* out, hipStream_t stream);
+hipError_t launch_table_hash(const void* q, size_t bytes, unsigned long long* out, hipStream_t stream);
 hipError_t launch_fdiv_check(int n, const float* a, const float* b, float* out, hipStream_t stream);
 hipError_t launch_fdiv64_check(int n, const double* a, const double* b, double* out, hipStream_t stream);
 hipError_t launch_prof_pack(int A, int T, const float* load_w, const float* pv_w, float2* prof,

@@ -2088,6 +2088,39 @@ __global__ void fdiv64_check_kernel(int n, const double* __restrict__ a, const d
 }
 #endif
 
+// Episode metrics of the context (community.py:179 avg_reward per scenario): out = {sum_s ep_reward[s],
+// S} in f64, one workgroup, a fixed reduction tree (deterministic), ready for the RCCL all-reduce.
+#if P2PMG_IN_PART(0)
+__global__ __launch_bounds__(256) void metrics_kernel(int S, const float* __restrict__ ep, double* __restrict__ out) {
+  __shared__ double sh[256];
+  double acc = 0.0;
+  for (int s = threadIdx.x; s < S; s += 256) acc += (double)ep[s];
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = sh[0];
+    out[1] = (double)S;
+  }
+}
+// Order-independent 64-bit fingerprint of a table's bit pattern (sum over words of a splitmix of
+// (word, index)): equal on every rank iff the replicas hold the same bits (up to hash collisions)
+__global__ void table_hash_kernel(const uint32_t* __restrict__ w, size_t n, unsigned long long* __restrict__ out) {
+  unsigned long long acc = 0;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    unsigned long long x = ((unsigned long long)w[k] << 32) ^ (k * 0x9E3779B97F4A7C15ull);
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    acc += x ^ (x >> 31);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+#endif
+
 // Standalone QActor calls, applied in order by a single thread (rl.py:89-129).
 template <typename QT>
 __global__ void q_calls_kernel(const QCallParams p) {
@@ -2337,6 +2370,21 @@ hipError_t launch_q_calls(const QCallParams& p, hipStream_t stream) {
     hipLaunchKernelGGL(q_calls_kernel<double>, dim3(1), dim3(64), 0, stream, p);
   else
     hipLaunchKernelGGL(q_calls_kernel<float>, dim3(1), dim3(64), 0, stream, p);
+  return hipGetLastError();
+}
+#endif
+
+#if P2PMG_IN_PART(0)
+hipError_t launch_metrics(int S, const float* ep, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(metrics_kernel, dim3(1), dim3(256), 0, stream, S, ep, out);
+  return hipGetLastError();
+}
+hipError_t launch_table_hash(const void* q, size_t bytes, unsigned long long* out, hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(out, 0, 8, stream);
+  if (e != hipSuccess) return e;
+  const size_t n = bytes / 4;
+  hipLaunchKernelGGL(table_hash_kernel, dim3((unsigned)std::min<size_t>(2048, grid_for(n, 256))), dim3(256), 0, stream,
+                     reinterpret_cast<const uint32_t*>(q), n, out);
   return hipGetLastError();
 }
 #endif

@@ -79,6 +79,8 @@ struct p2pmg_ctx {
   long long* qdelta = nullptr; // shared table deltas [kDeltaCopies][n_states][4]
   void* comm = nullptr;        // ncclComm_t
   int nranks = 1;
+  double* d_metrics = nullptr;           // [2] episode-metric sum and count (p2pmg_allreduce_metrics)
+  unsigned long long* d_hash = nullptr;  // [nranks] table fingerprints (p2pmg_table_hash_allgather)
   bool have_env = false, have_prof = false, have_params = false, have_codes = false;
   // DQN learner (config.learner = P2PMG_LEARNER_DQN)
   bool dqn = false;
@@ -119,6 +121,8 @@ struct Rccl {
   int (*allReduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;  // ncclDataType_t, ncclRedOp_t as int
   int (*commDestroy)(void*) = nullptr;
   const char* (*getErrorString)(int) = nullptr;
+  int (*allGather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
+  int (*commCount)(const void*, int*) = nullptr;
 };
 static Rccl* rccl() {
   static Rccl r;
@@ -136,6 +140,8 @@ static Rccl* rccl() {
       r.allReduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(r.h, "ncclAllReduce");
       r.commDestroy = (int (*)(void*))dlsym(r.h, "ncclCommDestroy");
       r.getErrorString = (const char* (*)(int))dlsym(r.h, "ncclGetErrorString");
+      r.allGather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(r.h, "ncclAllGather");
+      r.commCount = (int (*)(const void*, int*))dlsym(r.h, "ncclCommCount");
     }
   }
   return (r.h && r.getUniqueId && r.commInitRank && r.allReduce && r.commDestroy) ? &r : nullptr;
@@ -330,6 +336,8 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   if (c->dummy) (void)hipFree(c->dummy);
   if (c->rec_pack) (void)hipFree(c->rec_pack);
   dfree(c->ep_reward);
+  dfree(c->d_metrics);
+  dfree(c->d_hash);
   for (auto& b : c->rec_f32) dfree(b);
   dfree(c->rec_action);
   dfree(c->rec_index);
@@ -1098,6 +1106,55 @@ int p2pmg_allreduce_q_delta(p2pmg_ctx* c) {
   HIP_TRY(c, p2pmg::launch_fold_delta(c->qdelta, c->n_states * kQPad, c->stream));
   const int rc = r->allReduce(c->qdelta, c->qdelta, c->n_states * kQPad, 4, 0, c->comm, c->stream);
   if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclAllReduce: ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
+  return P2PMG_OK;
+}
+
+int p2pmg_comm_nranks(p2pmg_ctx* c, int* n) {
+  if (!c || !n) return P2PMG_E_INVALID;
+  if (!c->comm) {
+    *n = 1;  // no communicator: a world of one
+    return P2PMG_OK;
+  }
+  Rccl* r = rccl();
+  if (!r->commCount) return fail(c, P2PMG_E_UNSUPPORTED, "ncclCommCount not found");
+  const int rc = r->commCount(c->comm, n);
+  if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclCommCount: ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
+  return P2PMG_OK;
+}
+
+int p2pmg_allreduce_metrics(p2pmg_ctx* c, double* out) {
+  if (!c || !out) return P2PMG_E_INVALID;
+  if (!c->ep_reward) return fail(c, P2PMG_E_STATE, "allreduce_metrics: no episode launched");
+  if (!c->d_metrics) HIP_TRY(c, dmalloc(&c->d_metrics, 2));
+  HIP_TRY(c, p2pmg::launch_metrics(c->S, c->ep_reward, c->d_metrics, c->stream));
+  if (c->comm) {  // ncclFloat64 = 8, ncclSum = 0: sum and count over every rank (xGMI)
+    Rccl* r = rccl();
+    const int rc = r->allReduce(c->d_metrics, c->d_metrics, 2, 8, 0, c->comm, c->stream);
+    if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclAllReduce(metrics): ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
+  }
+  HIP_TRY(c, hipMemcpyAsync(out, c->d_metrics, 16, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return P2PMG_OK;
+}
+
+int p2pmg_table_hash_allgather(p2pmg_ctx* c, uint64_t* out) {
+  if (!c || !out) return P2PMG_E_INVALID;
+  if (!c->q) return fail(c, P2PMG_E_STATE, "table_hash: context has no Q-table");
+  const int n = c->comm ? c->nranks : 1;
+  if (n > 1024) return fail(c, P2PMG_E_UNSUPPORTED, "table_hash: more than 1024 ranks");
+  if (!c->d_hash) HIP_TRY(c, dmalloc(&c->d_hash, 1025));
+  const size_t bytes = (c->cfg.shared_q ? (size_t)1 : (size_t)c->A) * c->n_states * kQPad * c->q_elem;
+  HIP_TRY(c, p2pmg::launch_table_hash(c->q, bytes, c->d_hash + 1024, c->stream));
+  if (c->comm) {  // ncclUint64 = 5: every rank's fingerprint, in rank order
+    Rccl* r = rccl();
+    if (!r->allGather) return fail(c, P2PMG_E_UNSUPPORTED, "ncclAllGather not found");
+    const int rc = r->allGather(c->d_hash + 1024, c->d_hash, 1, 5, c->comm, c->stream);
+    if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclAllGather: ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
+  } else {
+    HIP_TRY(c, hipMemcpyAsync(c->d_hash, c->d_hash + 1024, 8, hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIP_TRY(c, hipMemcpyAsync(out, c->d_hash, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return P2PMG_OK;
 }
 

@@ -98,9 +98,10 @@ class ShardedTrainer:
     DeviceCommunityBatch interface; the default is the HIP engine.
 
     shared_q: one policy table for every agent of every scenario on every rank (config 3).
-    exchange: how the shared-table deltas are summed over ranks — "rccl" (device all-reduce over
-    xGMI, the production path), "host" (copy out, sum over the torch process group, copy back)
-    or "auto" (rccl when the process group is nccl/RCCL, host otherwise).
+    exchange: how the shared-table deltas and the episode metrics are summed over ranks — "rccl"
+    (device all-reduce over xGMI through the context's RCCL communicator, the production path),
+    "host" (copy out, sum over the torch process group, copy back) or "auto" (rccl when the
+    process group is nccl/RCCL, host otherwise).
     battery: kwargs for ``set_battery`` (scalars), enabling the storage rule."""
 
     def __init__(self, n_scenarios: int, n_agents: int = 2, rounds: int = 1, horizon: int = 96,
@@ -128,7 +129,7 @@ class ShardedTrainer:
         if battery is not None:
             self.eng.set_battery(**battery)
         self.exchange = None
-        if self.shared_q and world > 1:
+        if world > 1:
             if exchange == "auto":
                 import torch.distributed as dist
                 exchange = "rccl" if dist.is_initialized() and dist.get_backend() == "nccl" else "host"
@@ -158,11 +159,14 @@ class ShardedTrainer:
                              next_epsilon=next_epsilon)
         if self.shared_q:
             self.exchange_q_delta()
-        local = self.eng.episode_reward().astype(np.float64)
+        if self.exchange == "rccl":  # episode metrics over RCCL, reduced on the device
+            total, count = self.eng.allreduce_metrics()
+        else:
+            local = self.eng.episode_reward().astype(np.float64)
+            total, count = all_reduce_sum(np.array([local.sum(), local.size]), self.world)
         self.eng.reset_temperatures_philox(self.episode + 1, reset_sigma)
         self.episode += 1
-        tot = all_reduce_sum(np.array([local.sum(), local.size]), self.world)
-        return float(tot[0] / tot[1])
+        return float(total / count)
 
     def episode_rewards_global(self) -> np.ndarray:
         return all_gather_concat(self.eng.episode_reward(), self.world)

@@ -211,6 +211,25 @@ class DeviceCommunityBatch:
     def allreduce_q_delta(self):
         self._chk(self.L.p2pmg_allreduce_q_delta(self._ctx), "allreduce_q_delta")
 
+    def comm_nranks(self) -> int:
+        """Ranks of the RCCL communicator (1 without one)."""
+        n = C.c_int(0)
+        self._chk(self.L.p2pmg_comm_nranks(self._ctx, C.byref(n)), "comm_nranks")
+        return int(n.value)
+
+    def allreduce_metrics(self):
+        """(sum of the last episode's rewards over every rank's scenarios, scenario count): the
+        local sum on the device, then an RCCL all-reduce when a communicator exists."""
+        out = np.zeros(2, np.float64)
+        self._chk(self.L.p2pmg_allreduce_metrics(self._ctx, out.ctypes.data), "allreduce_metrics")
+        return float(out[0]), int(out[1])
+
+    def table_hash_allgather(self) -> np.ndarray:
+        """64-bit fingerprints of every rank's Q-table replica, in rank order (RCCL all-gather)."""
+        out = np.zeros(max(1, self.comm_nranks()), np.uint64)
+        self._chk(self.L.p2pmg_table_hash_allgather(self._ctx, out.ctypes.data), "table_hash_allgather")
+        return out
+
     # ----------------------------------------------------------------- the hot path
     def run_episode(self, mode: str = "train", rng: str = "replay", episode: int = 0, epsilon: float = 0.81,
                     record: Sequence[str] = (), philox: str = "auto", kernel: str = "auto",

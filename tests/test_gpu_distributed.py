@@ -98,3 +98,71 @@ def test_shared_table_two_ranks_match_single_context():
     assert np.count_nonzero(q1) > 0
     assert np.array_equal(per1, per2) and np.array_equal(q1, q2)
     assert np.allclose(means1, means2, rtol=0, atol=1e-9)
+
+
+def test_rccl_metrics_and_table_hash_world1():
+    """The RCCL pieces on one rank: a world-1 communicator, the metric all-reduce (= the local
+    sum of the episode rewards) and the table fingerprint all-gather (changes when the table does)."""
+    from p2pmicrogrid_amd.engine import comm_unique_id
+    tr = ShardedTrainer(301, 4, 1, 48, device=0, shared_q=True)
+    tr.eng.comm_init(comm_unique_id(), 0, 1)
+    assert tr.eng.comm_nranks() == 1
+    h0 = tr.eng.table_hash_allgather()
+    tr.eng.run_episode("train", "philox", episode=0, epsilon=0.5)
+    total, count = tr.eng.allreduce_metrics()
+    local = tr.eng.episode_reward().astype(np.float64)
+    assert count == 301 and abs(total - local.sum()) <= 1e-9 * abs(local).sum()
+    tr.eng.allreduce_q_delta()
+    tr.eng.apply_q_delta()
+    h1 = tr.eng.table_hash_allgather()
+    assert h0.shape == (1,) and h1[0] != h0[0]
+    assert tr.eng.table_hash_allgather()[0] == h1[0]
+    tr.eng.close()
+
+
+def _rccl_worker(rank, world, port, q, shared):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kw = dict(shared_q=True, battery=dict(capacity=4.0e6 * 3600)) if shared else {}
+    tr = ShardedTrainer(301, 4 if shared else 2, 1, 96, rank=rank, world=world, device=rank, exchange="rccl", **kw)
+    assert tr.eng.comm_nranks() == world
+    means = [tr.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    per = tr.episode_rewards_global()
+    hashes = tr.eng.table_hash_allgather() if shared else None
+    if rank == 0:
+        q.put((means, per, None if not shared else (tr.eng.get_q(0, 1), hashes)))
+    dist.barrier()
+    tr.eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("shared", [False, True])
+def test_two_ranks_over_rccl_match_single_context(shared):
+    """Two ranks on two GPUs with the deltas and metrics exchanged over RCCL (xGMI) reproduce the
+    single-context run; the shared table's replicas agree bit for bit (fingerprint all-gather)."""
+    from p2pmicrogrid_amd import _lib
+    if _lib.device_count() < 2:
+        pytest.skip("needs 2 visible GPUs (the driver's 8-GPU node runs this path through bench.py)")
+    kw = dict(shared_q=True, battery=dict(capacity=4.0e6 * 3600)) if shared else {}
+    single = ShardedTrainer(301, 4 if shared else 2, 1, 96, device=0, **kw)
+    means1 = [single.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    per1 = single.episode_rewards_global()
+    q1 = single.eng.get_q(0, 1) if shared else None
+    single.eng.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rccl_worker, args=(r, 2, port, q, shared)) for r in range(2)]
+    for p in procs:
+        p.start()
+    means2, per2, extra = q.get(timeout=500)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.array_equal(per1, per2)
+    assert np.allclose(means1, means2, rtol=0, atol=1e-9)
+    if shared:
+        q2, hashes = extra
+        assert np.array_equal(q1, q2) and hashes.shape == (2,) and hashes[0] == hashes[1]
