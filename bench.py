@@ -247,6 +247,7 @@ def main_dqn(args, rank, world, local, S, N, R, T):
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_dqn(args.cpu_seconds, R=R, T=T)
+            out["cpu_baseline"].update(os_cpu_count=os.cpu_count(), threads=1)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
@@ -291,6 +292,30 @@ def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 
     return {"value": S * N * T * eps_done / dt, "unit": "agent-steps/s", "cores": 1, "kind": "port",
             "sample": f"{S} scenarios x N={N} (R={R}, T={T}, {what}{q_dtype} Q), {eps_done} training episodes, "
                       f"oracle/restatement.py vectorised NumPy, {dt:.1f} s"}
+
+
+def cpu_baseline_per_object(seconds: float, N: int = 2, R: int = 1, T: int = 96):
+    """SURVEY.md §8(d) reference-shaped leg: oracle/scalar_loop.py, one object per agent and the
+    community.py:149-182 loop nesting (t -> round -> agent) in scalar float32, one thread,
+    exploration drawn from np.random in the reference's order, ε schedule of community.py:279-286."""
+    from oracle.scalar_loop import ScalarCommunity, ScalarQAgent
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    inp = scenario_batch(1, N, T)
+    agents = [ScalarQAgent(inp.load_w[0, i], inp.pv_w[0, i], inp.max_in[0, i], inp.t_in0[0, i], inp.t_m0[0, i])
+              for i in range(N)]
+    com = ScalarCommunity(agents, inp.time, inp.t_out[0], R)
+    rs = np.random.RandomState(42)
+    t0 = time.perf_counter()
+    done = 0
+    while True:
+        com.train_episode(rs=rs, eps=epsilon_at(done))
+        done += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": N * T * done / dt, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": f"1 scenario x N={N} (R={R}, T={T}), {done} training episodes, oracle/scalar_loop.py "
+                      f"per-object scalar loop (reference loop nesting), {dt:.1f} s"}
 
 
 def load_traffic(path: str, workload: str):
@@ -456,9 +481,14 @@ def main():
         if traffic:
             out["roofline"]["traffic_source"] = traffic.get("source")
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, S=(64 if hetero else 256) if N <= 4 else 64,
-                                               N=N, R=R, T=T, q_dtype=q_dtype, shared=shared, battery=battery,
-                                               hetero=hetero, t_sample=960 if T > 960 else 0)
+            cb = cpu_baseline(args.cpu_seconds, S=(64 if hetero else 256) if N <= 4 else 64,
+                              N=N, R=R, T=T, q_dtype=q_dtype, shared=shared, battery=battery,
+                              hetero=hetero, t_sample=960 if T > 960 else 0)
+            cb["os_cpu_count"] = os.cpu_count()
+            cb["threads"] = 1  # NumPy here runs single-threaded element-wise ops (no BLAS on this path)
+            if not (shared or battery or hetero):  # the per-object loop restates the tabular path only
+                cb["per_object"] = cpu_baseline_per_object(min(args.cpu_seconds, 5.0), N=N, R=R, T=T)
+            out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
