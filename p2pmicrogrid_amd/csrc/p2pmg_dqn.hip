@@ -2,7 +2,7 @@
 //   QNetwork rl.py:135-148, ActorModel rl.py:151-197, ReplayBuffer rl.py:200-248,
 //   Trainer._train / _soft_update rl.py:307-359, DQNAgent agent.py:301-350.
 //
-// One environment step = two launches (plus, for one shared network, a reduce and an Adam launch):
+// One environment step = two launches (plus, for one shared network, one reduce + Adam launch):
 //   dqn_act_kernel<N>    one workgroup per scenario, ONE WAVE PER AGENT; lane j is hidden unit j
 //                        of the agent's Q-MLP (weights streamed as coalesced 256-B rows), the
 //                        R+1 Jacobi rounds exchange the proposal matrix through LDS, then market,
@@ -559,43 +559,44 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   }
 }
 
-// shared network: sum the workgroup partials in a fixed order, in two levels so the sum is
-// parallel over both the 4609 parameters and the partials: level 1 (grid.y = kRedChunks) folds
-// each run of `per` consecutive partials sequentially into the run's first row, in place (one
-// thread owns one (run, parameter) cell); level 2 adds the runs' results in run order.
-constexpr int kRedChunks = 64;
-__global__ void dqn_reduce_chunks_kernel(const DqnParams d, int n_partials, int per) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  const int b0 = blockIdx.y * per;
-  if (k >= kDqnParams || b0 >= n_partials) return;
-  const int b1 = min(n_partials, b0 + per);
-  float* g = d.grad + k;
+// shared network, one launch: the partials' sum and (adam != 0) the Adam step.  A 1024-thread
+// workgroup owns 64 parameters; its 16 waves each fold a contiguous run of the partials in partial
+// order (8 loads in flight), and wave 0 adds the 16 runs in run order — a fixed order, so every
+// launch gives the same sum.  adam == 0 leaves the sum in gsum for the cross-rank all-reduce.
+constexpr int kRedParams = 64, kRedSlices = 16;
+__global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kernel(const DqnParams d, int n_partials,
+                                                                               int adam) {
+  __shared__ float part[kRedSlices][kRedParams];
+  const int j = threadIdx.x % kRedParams, sl = threadIdx.x / kRedParams;
+  const int k = blockIdx.x * kRedParams + j;
+  const int per = (n_partials + kRedSlices - 1) / kRedSlices;
+  const int b0 = sl * per, b1 = min(n_partials, b0 + per);
   float s = 0.0f;
-  int b = b0;
-  for (; b + 8 <= b1; b += 8) {  // 8 loads in flight, the sum still in partial order
-    float v[8];
+  if (k < kDqnParams) {
+    const float* g = d.grad + k;
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {
+      float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = g[(size_t)(b + u) * kNetStride];
+      for (int u = 0; u < 8; ++u) v[u] = g[(size_t)(b + u) * kNetStride];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < b1; ++b) s += g[(size_t)b * kNetStride];
   }
-  for (; b < b1; ++b) s += g[(size_t)b * kNetStride];
-  g[(size_t)b0 * kNetStride] = s;
-}
-__global__ void dqn_reduce_kernel(const DqnParams d, int n_partials, int per) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= kDqnParams) return;
-  float s = 0.0f;
-  int b = 0;
-  for (; b + 8 * per <= n_partials; b += 8 * per) {
-    float v[8];
+  part[sl][j] = s;
+  __syncthreads();
+  if (sl != 0 || k >= kDqnParams) return;
+  float t = part[0][j];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = d.grad[(size_t)(b + u * per) * kNetStride + k];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
+  for (int r = 1; r < kRedSlices; ++r) t += part[r][j];
+  if (!adam) {
+    d.gsum[k] = t;
+    return;
   }
-  for (; b < n_partials; b += per) s += d.grad[(size_t)b * kNetStride + k];
-  d.gsum[k] = s;
+  float gk = t * d.inv_agents;
+  if (k < kOffB1) gk = fminf(fmaxf(gk, -d.clip), d.clip);
+  adam_update(d, d.theta, d.target, d.adam_m, d.adam_v, k, gk, d.lr_t);
 }
 
 // shared network: mean over every agent (all ranks after the all-reduce), clip, Adam, soft update
@@ -661,13 +662,9 @@ hipError_t launch_dqn_sample(const DqnParams& d, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_dqn_reduce(const DqnParams& d, int n_partials, hipStream_t st) {
-  const int per = (n_partials + kRedChunks - 1) / kRedChunks;
-  if (per > 1) {
-    hipLaunchKernelGGL(dqn_reduce_chunks_kernel, dim3((kDqnParams + 255) / 256, kRedChunks), dim3(256), 0, st, d,
-                       n_partials, per);
-  }
-  hipLaunchKernelGGL(dqn_reduce_kernel, dim3((kDqnParams + 255) / 256), dim3(256), 0, st, d, n_partials, per);
+hipError_t launch_dqn_reduce_adam(const DqnParams& d, int n_partials, bool adam, hipStream_t st) {
+  hipLaunchKernelGGL(dqn_reduce_adam_kernel, dim3((kDqnParams + kRedParams - 1) / kRedParams),
+                     dim3(kRedParams * kRedSlices), 0, st, d, n_partials, adam ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -99,7 +99,8 @@ struct DqnParams {
 hipError_t launch_dqn_act(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_sample(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_train(const DqnParams& p, int blocks, bool shared_partials, hipStream_t stream);
-hipError_t launch_dqn_reduce(const DqnParams& p, int n_partials, hipStream_t stream);
+// sum of the train workgroups' partials (+ adam: the Adam step on it; else the sum goes to gsum)
+hipError_t launch_dqn_reduce_adam(const DqnParams& p, int n_partials, bool adam, hipStream_t stream);
 hipError_t launch_dqn_adam_shared(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_forward(const float* theta, int n, const float* x, float* q, hipStream_t stream);
 

@@ -1451,14 +1451,15 @@ static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d) {
   HIP_TRY(c, p2pmg::launch_dqn_sample(d, c->stream));
   if (c->n_nets == 1) {
     HIP_TRY(c, p2pmg::launch_dqn_train(d, c->d_blocks, true, c->stream));
-    HIP_TRY(c, p2pmg::launch_dqn_reduce(d, c->d_blocks, c->stream));
-    if (c->comm && c->nranks > 1) {
+    const bool ranks = c->comm && c->nranks > 1;
+    HIP_TRY(c, p2pmg::launch_dqn_reduce_adam(d, c->d_blocks, !ranks, c->stream));  // one rank: sum + Adam
+    if (ranks) {
       Rccl* r = rccl();
       // ncclFloat32 = 7, ncclSum = 0: gradient sum over ranks (xGMI), 4609 floats
       const int rc = r->allReduce(c->d_gsum, c->d_gsum, p2pmg::kDqnParams, 7, 0, c->comm, c->stream);
       if (rc != 0) return fail(c, P2PMG_E_HIP, "dqn gradient all-reduce failed");
+      HIP_TRY(c, p2pmg::launch_dqn_adam_shared(d, c->stream));
     }
-    HIP_TRY(c, p2pmg::launch_dqn_adam_shared(d, c->stream));
   } else {
     HIP_TRY(c, p2pmg::launch_dqn_train(d, c->A, false, c->stream));
   }
