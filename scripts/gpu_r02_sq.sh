@@ -22,4 +22,4 @@ for W in config2 config3; do
     timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace -d "$O/${W}_$P" -o p --output-format csv -- python3 "$R/bench.py" --workload $W --steps $ST --warmup 1 --no-cpu-baseline > "$O/${W}_$P.log" 2>&1 || { tail -20 "$O/${W}_$P.log"; exit 1; }
   done
 done
-python3 "$R/scripts/summarize_sq.py" "$O" > "$O/sq_summary.json" && cat "$O/sq_summary.json"
+mkdir -p "$O/sq" && python3 "$R/scripts/summarize_sq.py" "$O" "$O/sq" > "$O/sq_summary.json" && cat "$O/sq_summary.json"

@@ -1,5 +1,8 @@
 """Per-launch averages of the SQ counter passes written by scripts/gpu_r02_sq.sh.
 
+usage: summarize_sq.py <gpurun_out dir> [<dest dir>]  (dest: one sq_<workload>.json per workload,
+which bench.py reads for roofline.issue)
+
 For each workload, the episode kernel's counters (first launch dropped as warm-up) averaged over
 launches, plus derived figures: SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles
 (MI355X_MICROARCH.md constants table), so cycles = 4 x counter."""
@@ -45,5 +48,9 @@ for w, kname in KERNEL.items():
         # one wave alone issues a VALU every 4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost')
         "valu_issue_frac_of_one_wave_peak": (4 * d.get("SQ_INSTS_VALU", 0) / (4 * wc)) if wc else None,
     }
-    res[w] = {"kernel": kname, "counters_per_launch": d, "derived": der}
+    res[w] = {"kernel": kname, "workload": w, "counters_per_launch": d, "derived": der,
+              "source": "scripts/gpu_r02_sq.sh (rocprofv3 --pmc, two passes of <= 8 SQ counters, P2PMG_NO_SPEC=1)"}
+    if len(sys.argv) > 2:
+        with open(os.path.join(sys.argv[2], f"sq_{w}.json"), "w") as fh:
+            json.dump(res[w], fh, indent=1)
 print(json.dumps(res, indent=1))
