@@ -320,16 +320,18 @@ def cpu_baseline_per_object(seconds: float, N: int = 2, R: int = 1, T: int = 96)
 
 CLOCK_GHZ = 2.4          # MI355X peak engine clock
 SIMDS = 256 * 4          # 256 CUs x 4 SIMDs
-# MI355X_MICROARCH.md 'vector-instruction ISSUE cost': a SIMD retires a wave64 v_add/v_fma every 2
-# cycles with two or more waves resident, every 4 cycles when one wave issues alone
-VALU_PEAK_G = SIMDS * CLOCK_GHZ / 2
+# A SIMD is 16 lanes wide: a wave64 VALU instruction occupies it for one quad-cycle (the SQ counts
+# SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU quad-cycles; the f32 vector peak of 157 TF counts packed
+# v_pk_fma_f32, two FMAs per lane).  Chip peak: one wave-instruction per SIMD per 4 cycles; a wave
+# that has its SIMD to itself issues at most that too (MI355X_MICROARCH.md 'ISSUE cost': 4 cycles).
+VALU_PEAK_G = SIMDS * CLOCK_GHZ / 4
 ONE_WAVE_PEAK_G = CLOCK_GHZ / 4
 
 
 def issue_roofline(workload: str, kernel_ms: float):
     """Instruction-issue roofline of the episode kernel: the VALU wave-instructions one launch
     issues (SQ_INSTS_VALU from the committed rocprofv3 counter pass, profiles/sq_<workload>.json,
-    scripts/gpu_r02_sq.sh) over the live kernel time, against the chip's VALU issue peak and,
+    scripts/gpu_sq_counters.sh) over the live kernel time, against the chip's VALU issue peak and,
     when every wave has a SIMD to itself, against that wave's own issue ceiling."""
     path = os.path.join(ROOT, "profiles", f"sq_{workload}.json")
     if not os.path.exists(path) or not kernel_ms == kernel_ms:

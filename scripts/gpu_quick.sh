@@ -1,7 +1,7 @@
 #!/bin/bash
 # quick device check: GPU tests (optional), the default bench line and the config3 bench line
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
-O="$R/gpurun_out/r02q"; mkdir -p "$O"
+O="$R/gpurun_out/quick"; mkdir -p "$O"
 if [ "${1:-tests}" = tests ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -40 "$O/pytest.log"; exit 1; }
 tail -2 "$O/pytest.log"

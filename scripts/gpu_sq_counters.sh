@@ -3,7 +3,7 @@
 # counters, separate runs) for the configs[1] fast kernel and the configs[2] sq16 kernel.
 # P2PMG_NO_SPEC=1 drops the fast kernel's producer blocks so its counters are the episode's own.
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
-O="$R/gpurun_out/r02sq"; mkdir -p "$O"
+O="$R/gpurun_out/sq"; mkdir -p "$O"
 WHAT="${1:-all}"
 if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -40 "$O/pytest.log"; exit 1; }

@@ -1,4 +1,4 @@
-"""Per-launch averages of the SQ counter passes written by scripts/gpu_r02_sq.sh.
+"""Per-launch averages of the SQ counter passes written by scripts/gpu_sq_counters.sh.
 
 usage: summarize_sq.py <gpurun_out dir> [<dest dir>]  (dest: one sq_<workload>.json per workload,
 which bench.py reads for roofline.issue)
@@ -49,7 +49,7 @@ for w, kname in KERNEL.items():
         "valu_issue_frac_of_one_wave_peak": (4 * d.get("SQ_INSTS_VALU", 0) / (4 * wc)) if wc else None,
     }
     res[w] = {"kernel": kname, "workload": w, "counters_per_launch": d, "derived": der,
-              "source": "scripts/gpu_r02_sq.sh (rocprofv3 --pmc, two passes of <= 8 SQ counters, P2PMG_NO_SPEC=1)"}
+              "source": "scripts/gpu_sq_counters.sh (rocprofv3 --pmc, two passes of <= 8 SQ counters, P2PMG_NO_SPEC=1)"}
     if len(sys.argv) > 2:
         with open(os.path.join(sys.argv[2], f"sq_{w}.json"), "w") as fh:
             json.dump(res[w], fh, indent=1)
