@@ -12,7 +12,8 @@
 //                        is shared): samples 32 transitions, target forward over the 96 rows
 //                        (ns x 3 action values), online forward + backward over the 32 rows, all
 //                        on v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulation); wave w
-//                        owns output columns 16w..16w+15 of every 64-wide layer.  Per-agent
+//                        owns hidden units 16w..16w+15 of both 64-wide layers (layer 2 as the
+//                        transposed product, so layer 3 reduces in-lane).  Per-agent
 //                        networks: clip + Adam + soft update fused in the epilogue; shared: the
 //                        workgroup's gradient sum is written as a partial.
 // Layouts (HBM): networks [n_nets][4672] f32 (Keras order W1[5][64] b1 W2[64][64] b2 W3[64] b3),
@@ -293,22 +294,27 @@ __device__ __forceinline__ void batch_put(float* dst, int t, float v0, float v1)
   if (k < kTrans - 8) dst[b * kTrans + k + 8] = v1;
 }
 
-// the weights one train workgroup reads, per lane (wave w owns columns 16w..16w+15)
-// (per-agent networks read W2 per MFMA step from L1/L2; a shared network stages it in LDS)
+// the weights one train workgroup reads, per lane (layer 1 and dH1: column col of wave w;
+// layers 2 and 3: the 4 hidden units 16 w + 4 g4 + r of the transposed tiles).  Per-agent networks
+// read W2 per MFMA step from L1/L2; a shared network stages it in LDS.
 struct TrainW {
-  float bt0, bo0, bt1, bo1, b1t, b1o, b2t, w3t, b2o, w3o, b3t, b3o;
+  float bt0, bo0, bt1, bo1, b1t, b1o, b3t, b3o;
+  float b2t[4], w3t[4], b2o[4], w3o[4];  // layer 2/3 of the hidden units 16 w + 4 g4 + r
 };
-__device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const float* tg, int col, int g4) {
+__device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const float* tg, int col, int g4, int h0) {
   W.bt0 = tg[kOffW1 + g4 * kH + col];
   W.bo0 = th[kOffW1 + g4 * kH + col];
   W.bt1 = g4 == 0 ? tg[kOffW1 + 4 * kH + col] : 0.0f;
   W.bo1 = g4 == 0 ? th[kOffW1 + 4 * kH + col] : 0.0f;
   W.b1t = tg[kOffB1 + col];
   W.b1o = th[kOffB1 + col];
-  W.b2t = tg[kOffB2 + col];
-  W.w3t = tg[kOffW3 + col];
-  W.b2o = th[kOffB2 + col];
-  W.w3o = th[kOffW3 + col];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    W.b2t[r] = tg[kOffB2 + h0 + r];
+    W.w3t[r] = tg[kOffW3 + h0 + r];
+    W.b2o[r] = th[kOffB2 + h0 + r];
+    W.w3o[r] = th[kOffW3 + h0 + r];
+  }
   W.b3t = tg[kOffB3];
   W.b3o = th[kOffB3];
 }
@@ -320,30 +326,32 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   __shared__ float smpb[2][kB * kTrans];  // this agent's batch and the next one's (prefetched)
   __shared__ float H1t[3 * kB][kLdsRow];
   __shared__ float H1o[kB][kLdsRow];
-  __shared__ float dZ2[kB][kLdsRow];
+  __shared__ __attribute__((aligned(16))) float dZ2[kB][kLdsRow];
   __shared__ float qpart[4][4 * kB];  // per-wave partial Q: rows 0..95 target (action x sample), 96..127 online
   // one shared network: W2 (target, online) staged in LDS once per workgroup, element (k, j) at
-  // k*64 + (j ^ w2_swz(k)), conflict-free both for the forward's B operand (row k = 4 kk + g4,
+  // k*64 + (j ^ w2_swz(k)), conflict-free both for layer 2's weight operand (row k = 4 kk + g4,
   // column j = col) and for dH1's W2^T read (row k = col, column j = 4 kk + g4)
   __shared__ float W2s[SHARED ? 2 : 1][SHARED ? kH * kH : 1];
   const EpisodeParams& p = d.e;
   const int w = threadIdx.x / kWave, l = threadIdx.x % kWave;
   const int c16 = l & 15, g4 = l >> 4;
-  const int col = 16 * w + c16;  // this lane's column of every 64-wide layer
+  const int col = 16 * w + c16;     // this lane's column of layer 1 and of dH1
+  const int h0 = 16 * w + 4 * g4;   // this lane's 4 hidden units of layer 2 (transposed tiles)
   const size_t A = (size_t)p.A;
 
   f32x4 gW2[4], gW1;
 #pragma unroll
   for (int m = 0; m < 4; ++m) gW2[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   gW1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  float gb1 = 0.0f, gb2 = 0.0f, gW3 = 0.0f, gb3 = 0.0f;
+  float gb1 = 0.0f, gb3 = 0.0f;
+  float gb2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gW3[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   const int n_ag = d.batch ? 1 : d.apb;
   int net = d.batch ? d.net : 0;
   TrainW W;
   if constexpr (SHARED) {
     const float* th0 = d.theta + (size_t)net * kNetStride;
     const float* tg0 = d.target + (size_t)net * kNetStride;
-    load_train_w(W, th0, tg0, col, g4);
+    load_train_w(W, th0, tg0, col, g4, h0);
     for (int e = threadIdx.x; e < kH * kH; e += 256) {
       const int k = e / kH, j = e % kH;
       W2s[0][k * kH + (j ^ w2_swz(k))] = tg0[kOffW2 + e];
@@ -367,7 +375,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     net = d.batch ? d.net : (SHARED ? 0 : a);
     const float* th = d.theta + (size_t)net * kNetStride;
     const float* tg = d.target + (size_t)net * kNetStride;
-    if (!SHARED) load_train_w(W, th, tg, col, g4);
+    if (!SHARED) load_train_w(W, th, tg, col, g4, h0);
     float (*smp)[kTrans] = reinterpret_cast<float (*)[kTrans]>(smpb[ag & 1]);
     // prefetch the next agent's batch into registers; it goes to the other buffer at the end
     const bool has_next = !d.batch && ag + 1 < n_ag && a + 1 < (int)A;
@@ -402,7 +410,10 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     }
     __syncthreads();
 
-    // ---- layer 2: Z2 = H1 W2 + b2 (K = 64)
+    // ---- layer 2 as Z2^T = W2^T H1^T (K = 64): the operands of H1 W2 with the MFMA's A and B
+    // swapped, so the accumulator of row tile rt holds data row 16 rt + c16 at the hidden units
+    // h0 + r.  Layer 3 then sums 4 units in-lane and the 4 row groups with two exchanges, instead
+    // of a 16-lane butterfly per (row, unit).
     f32x4 at[6], ao[2];
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt) at[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -413,57 +424,59 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       const float bt = SHARED ? W2s[0][k * kH + (col ^ w2_swz(k))] : tg[kOffW2 + k * kH + col];
       const float bo = SHARED ? W2s[SHARED ? 1 : 0][k * kH + (col ^ w2_swz(k))] : th[kOffW2 + k * kH + col];
 #pragma unroll
-      for (int rt = 0; rt < 6; ++rt) at[rt] = mfma4(H1t[16 * rt + c16][k], bt, at[rt]);
-      ao[0] = mfma4(H1o[c16][k], bo, ao[0]);
-      ao[1] = mfma4(H1o[16 + c16][k], bo, ao[1]);
+      for (int rt = 0; rt < 6; ++rt) at[rt] = mfma4(bt, H1t[16 * rt + c16][k], at[rt]);
+      ao[0] = mfma4(bo, H1o[c16][k], ao[0]);
+      ao[1] = mfma4(bo, H1o[16 + c16][k], ao[1]);
     }
-    const float b2t = W.b2t, w3t = W.w3t, b2o = W.b2o, w3o = W.w3o;
+    // ---- layer 3, this wave's 16 units: in-lane over r, then over the 4 row groups (g4)
 #pragma unroll
-    for (int rt = 0; rt < 6; ++rt)
+    for (int rt = 0; rt < 6; ++rt) {
+      float s = 0.0f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float qp = sum16(relu(at[rt][r] + b2t) * w3t);
-        if (c16 == 0) qpart[w][16 * rt + 4 * g4 + r] = qp;
-      }
+      for (int r = 0; r < 4; ++r) s = s + relu(at[rt][r] + W.b2t[r]) * W.w3t[r];
+      s = sum_groups(s);
+      if (g4 == 0) qpart[w][16 * rt + c16] = s;
+    }
     float h2o[2][4];
     unsigned z2mask = 0;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < 2; ++rt) {
+      float s = 0.0f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float z = ao[rt][r] + b2o;
+        const float z = ao[rt][r] + W.b2o[r];
         h2o[rt][r] = relu(z);
         if (z > 0.0f) z2mask |= 1u << (4 * rt + r);
-        const float qp = sum16(h2o[rt][r] * w3o);
-        if (c16 == 0) qpart[w][3 * kB + 16 * rt + 4 * g4 + r] = qp;
+        s = s + h2o[rt][r] * W.w3o[r];
       }
+      s = sum_groups(s);
+      if (g4 == 0) qpart[w][3 * kB + 16 * rt + c16] = s;
+    }
     __syncthreads();
 
-    // ---- targets y = r + gamma * max_a' Q_target(ns, a') and dL/dq (rl.py:314-331)
-    const float b3t = W.b3t, b3o = W.b3o;
-    float dq[2][4];
+    // ---- targets y = r + gamma * max_a' Q_target(ns, a') and dL/dq (rl.py:314-331), for this
+    // lane's data rows b = 16 rt + c16
+    float dq[2];
     float lsum = 0.0f, dqsum = 0.0f;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < 2; ++rt) {
+      const int b = 16 * rt + c16;
+      float qt[3];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = 16 * rt + 4 * g4 + r;
-        float qt[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int row = k * kB + b;
-          qt[k] = (((qpart[0][row] + qpart[1][row]) + qpart[2][row]) + qpart[3][row]) + b3t;
-        }
-        const int ro = 3 * kB + b;
-        const float q = (((qpart[0][ro] + qpart[1][ro]) + qpart[2][ro]) + qpart[3][ro]) + b3o;
-        const float y = smp[b][5] + d.gamma * fmaxf(fmaxf(qt[0], qt[1]), qt[2]);
-        const float diff = q - y;
-        dq[rt][r] = (2.0f / (float)kB) * diff;
-        lsum += diff * diff;
-        dqsum += dq[rt][r];
+      for (int k = 0; k < 3; ++k) {
+        const int row = k * kB + b;
+        qt[k] = (((qpart[0][row] + qpart[1][row]) + qpart[2][row]) + qpart[3][row]) + W.b3t;
       }
-    if (w == 0) {  // loss = mean (y - q)^2; lanes with c16 == 0 hold disjoint rows
-      const float ls = sum_groups(lsum), dqs = sum_groups(dqsum);
+      const int ro = 3 * kB + b;
+      const float q = (((qpart[0][ro] + qpart[1][ro]) + qpart[2][ro]) + qpart[3][ro]) + W.b3o;
+      const float y = smp[b][5] + d.gamma * fmaxf(fmaxf(qt[0], qt[1]), qt[2]);
+      const float diff = q - y;
+      dq[rt] = (2.0f / (float)kB) * diff;
+      lsum += diff * diff;
+      dqsum += dq[rt];
+    }
+    if (w == 0) {  // loss = mean (y - q)^2: the 16 lanes of a row group hold the 32 rows
+      const float ls = sum16(lsum), dqs = sum16(dqsum);
       if (l == 0) {
         const float loss = ls / (float)kB;
         if (d.batch) d.loss_out[0] = loss;
@@ -472,26 +485,31 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       }
     }
 
-    // ---- backward (own columns)
-    float dz2[2][4];
+    // ---- backward: dZ2 of this lane's (row, units), stored row-major for dW2 and dH1
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      float dz2[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool on = (z2mask >> (4 * rt + r)) & 1u;
+        dz2[r] = on ? dq[rt] * W.w3o[r] : 0.0f;
+        gW3[r] += h2o[rt][r] * dq[rt];
+        gb2[r] += dz2[r];
+      }
+      *reinterpret_cast<float4*>(&dZ2[16 * rt + c16][h0]) = make_float4(dz2[0], dz2[1], dz2[2], dz2[3]);
+    }
+    __syncthreads();
+    // dW2 = H1^T dZ2 (K = the 32 data rows), accumulator rows = layer-1 units 16 mt + 4 g4 + r,
+    // columns = the wave's layer-2 units col
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool on = (z2mask >> (4 * rt + r)) & 1u;
-        dz2[rt][r] = on ? dq[rt][r] * w3o : 0.0f;
-        gW3 += h2o[rt][r] * dq[rt][r];
-        gb2 += dz2[rt][r];
-        dZ2[16 * rt + 4 * g4 + r][col] = dz2[rt][r];
+        const int b = 16 * rt + 4 * g4 + r;
+        const float dzb = dZ2[b][col];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) gW2[mt] = mfma4(H1o[b][16 * mt + c16], dzb, gW2[mt]);
       }
-    // dW2 = H1^T dZ2: the accumulator rows of dz2 are the K index (b = 16 rt + 4 g4 + r)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) gW2[mt] = mfma4(H1o[16 * rt + 4 * g4 + r][16 * mt + c16], dz2[rt][r], gW2[mt]);
-    __syncthreads();
     // dH1 = dZ2 W2^T (own columns m = col), then dZ1 = dH1 * [z1 > 0]; dW1 = X^T dZ1
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
@@ -515,8 +533,11 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   }
 
   gb1 = sum_groups(gb1);
-  gb2 = sum_groups(gb2);
-  gW3 = sum_groups(gW3);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {  // over the 16 data-row lanes of each row group
+    gb2[r] = sum16(gb2[r]);
+    gW3[r] = sum16(gW3[r]);
+  }
   const int net_out = net;
   if constexpr (!SHARED) {
     // Trainer._train epilogue: clip the first kernel's gradient, Adam, then update_targets
@@ -535,10 +556,13 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       const int k = 4 * g4 + r;
       if (k < 5) adam_update(d, th, tg, mm, vv, kOffW1 + k * kH + col, fminf(fmaxf(gW1[r], -d.clip), d.clip), lr);
     }
-    if (g4 == 0) {
-      adam_update(d, th, tg, mm, vv, kOffB1 + col, gb1, lr);
-      adam_update(d, th, tg, mm, vv, kOffB2 + col, gb2, lr);
-      adam_update(d, th, tg, mm, vv, kOffW3 + col, gW3, lr);
+    if (g4 == 0) adam_update(d, th, tg, mm, vv, kOffB1 + col, gb1, lr);
+    if (c16 == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        adam_update(d, th, tg, mm, vv, kOffB2 + h0 + r, gb2[r], lr);
+        adam_update(d, th, tg, mm, vv, kOffW3 + h0 + r, gW3[r], lr);
+      }
     }
     if (threadIdx.x == 0) adam_update(d, th, tg, mm, vv, kOffB3, gb3, lr);
   } else {
@@ -550,10 +574,13 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (4 * g4 + r < 5) gp[kOffW1 + (4 * g4 + r) * kH + col] = gW1[r];
-    if (g4 == 0) {
-      gp[kOffB1 + col] = gb1;
-      gp[kOffB2 + col] = gb2;
-      gp[kOffW3 + col] = gW3;
+    if (g4 == 0) gp[kOffB1 + col] = gb1;
+    if (c16 == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gp[kOffB2 + h0 + r] = gb2[r];
+        gp[kOffW3 + h0 + r] = gW3[r];
+      }
     }
     if (threadIdx.x == 0) gp[kOffB3] = gb3;
   }
