@@ -296,7 +296,7 @@ __device__ __forceinline__ void batch_put(float* dst, int t, float v0, float v1)
 
 // the weights one train workgroup reads, per lane (layer 1 and dH1: column col of wave w;
 // layers 2 and 3: the 4 hidden units 16 w + 4 g4 + r of the transposed tiles).  Per-agent networks
-// read W2 per MFMA step from L1/L2; a shared network stages it in LDS.
+// read W2 per MFMA step from L1/L2; a shared network keeps its 48 W2 operands in registers.
 struct TrainW {
   float bt0, bo0, bt1, bo1, b1t, b1o, b3t, b3o;
   float b2t[4], w3t[4], b2o[4], w3o[4];  // layer 2/3 of the hidden units 16 w + 4 g4 + r
@@ -319,8 +319,6 @@ __device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const f
   W.b3o = th[kOffB3];
 }
 
-__device__ __forceinline__ int w2_swz(int k) { return ((k & 3) << 4) | (((k >> 2) & 3) << 2); }
-
 template <bool SHARED>
 __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) {  // 2 waves / SIMD
   __shared__ float smpb[2][kB * kTrans];  // this agent's batch and the next one's (prefetched)
@@ -328,10 +326,6 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   __shared__ float H1o[kB][kLdsRow];
   __shared__ __attribute__((aligned(16))) float dZ2[kB][kLdsRow];
   __shared__ float qpart[4][4 * kB];  // per-wave partial Q: rows 0..95 target (action x sample), 96..127 online
-  // one shared network: W2 (target, online) staged in LDS once per workgroup, element (k, j) at
-  // k*64 + (j ^ w2_swz(k)), conflict-free both for layer 2's weight operand (row k = 4 kk + g4,
-  // column j = col) and for dH1's W2^T read (row k = col, column j = 4 kk + g4)
-  __shared__ float W2s[SHARED ? 2 : 1][SHARED ? kH * kH : 1];
   const EpisodeParams& p = d.e;
   const int w = threadIdx.x / kWave, l = threadIdx.x % kWave;
   const int c16 = l & 15, g4 = l >> 4;
@@ -348,14 +342,18 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   const int n_ag = d.batch ? 1 : d.apb;
   int net = d.batch ? d.net : 0;
   TrainW W;
+  // one shared network: the lane's 48 W2 operands (layer 2: W2[4 kk + g4][col] of the target and
+  // the online network; dH1: W2[col][4 kk + g4]) stay in registers for the whole launch
+  float w2t[SHARED ? 16 : 1], w2o[SHARED ? 16 : 1], w2c[SHARED ? 16 : 1];
   if constexpr (SHARED) {
     const float* th0 = d.theta + (size_t)net * kNetStride;
     const float* tg0 = d.target + (size_t)net * kNetStride;
     load_train_w(W, th0, tg0, col, g4, h0);
-    for (int e = threadIdx.x; e < kH * kH; e += 256) {
-      const int k = e / kH, j = e % kH;
-      W2s[0][k * kH + (j ^ w2_swz(k))] = tg0[kOffW2 + e];
-      W2s[SHARED ? 1 : 0][k * kH + (j ^ w2_swz(k))] = th0[kOffW2 + e];
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      w2t[kk] = tg0[kOffW2 + (4 * kk + g4) * kH + col];
+      w2o[kk] = th0[kOffW2 + (4 * kk + g4) * kH + col];
+      w2c[kk] = th0[kOffW2 + col * kH + 4 * kk + g4];
     }
   }
   // the first agent's batch (explicit batch, or the sample pre-pass output)
@@ -421,8 +419,8 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const int k = 4 * kk + g4;
-      const float bt = SHARED ? W2s[0][k * kH + (col ^ w2_swz(k))] : tg[kOffW2 + k * kH + col];
-      const float bo = SHARED ? W2s[SHARED ? 1 : 0][k * kH + (col ^ w2_swz(k))] : th[kOffW2 + k * kH + col];
+      const float bt = SHARED ? w2t[SHARED ? kk : 0] : tg[kOffW2 + k * kH + col];
+      const float bo = SHARED ? w2o[SHARED ? kk : 0] : th[kOffW2 + k * kH + col];
 #pragma unroll
       for (int rt = 0; rt < 6; ++rt) at[rt] = mfma4(bt, H1t[16 * rt + c16][k], at[rt]);
       ao[0] = mfma4(bo, H1o[c16][k], ao[0]);
@@ -517,7 +515,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
 #pragma unroll
       for (int kk = 0; kk < 16; ++kk) {
         const int j = 4 * kk + g4;
-        acc = mfma4(dZ2[16 * rt + c16][j], SHARED ? W2s[SHARED ? 1 : 0][col * kH + (j ^ w2_swz(col))] : th[kOffW2 + col * kH + j], acc);
+        acc = mfma4(dZ2[16 * rt + c16][j], SHARED ? w2c[SHARED ? kk : 0] : th[kOffW2 + col * kH + j], acc);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
