@@ -174,8 +174,7 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const float pij = P[i * N + j], pji = P[j * N + i];
-    const float si = sgn(pij);
-    const float ex = (si != sgn(pji)) ? si * fminf(fabsf(pij), fabsf(pji)) : 0.0f;
+    const float ex = __builtin_amdgcn_fmed3f(pij, -pji, 0.0f);  // pair_exchange (p2pmg_kernels.hip)
     g = g + (pij - ex);
     pp = pp + ex;
   }

@@ -379,12 +379,15 @@ __device__ __forceinline__ Row4<QT> patched(Row4<QT> r, uint32_t addr, const Pat
 // a global load + vmcnt(0) on the critical path)
 __device__ __forceinline__ float hp_of(const float4& lv, int act) { return sel3(act, lv.x, lv.y, lv.z); }
 
-// min(|a|, |b|) as one v_min_f32 with abs modifiers (written as C++, hipcc first canonicalises each
-// operand with a v_max; operands here are never NaN, so the plain v_min is the same value)
-__device__ __forceinline__ float min_abs(float a, float b) {
-  float r;
-  asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
-  return r;
+// community.py:45-54's bilateral exchange of one pair, sign(pij) * min(|pij|, |pji|) where the
+// signs differ and 0 where they agree, as ONE v_med3(pij, -pji, 0): with opposite signs pij and
+// -pji share a sign and the median of {0, pij, -pji} is the one nearer 0 (min for positives, max
+// for negatives); with equal signs 0 lies between them.  Where the reference's value is 0 the
+// median may be -0 instead of +0 (and vice versa): the market sums g and pp start at +0, and
+// adding a zero of either sign to a sum that starts at +0 never changes its value, so g, pp and
+// everything downstream are the same.  (Operands are never NaN.)
+__device__ __forceinline__ float pair_exchange(float pij, float pji) {
+  return __builtin_amdgcn_fmed3f(pij, -pji, 0.0f);
 }
 
 // ----------------------------------------------------------------- the episode kernel
@@ -645,8 +648,7 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const float pij = row[j], pji = col[j];
-      const float si = sgn(pij);
-      const float ex = (si != sgn(pji)) ? si * fminf(fabsf(pij), fabsf(pji)) : 0.0f;
+      const float ex = pair_exchange(pij, pji);
       g = g + (pij - ex);
       pp = pp + ex;
     }
@@ -1332,13 +1334,9 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     float g = 0.0f, pp = 0.0f;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      // ex = sign(pij) * min(|pij|, |pji|) where the signs differ (community.py:48-50).  With a
-      // zero operand min(...) = 0, so ex = +-0 and g, pp (which start at +0) take the same values
-      // as with the reference's 0; otherwise "signs differ" is "sign bits differ".
+      // ex = sign(pij) * min(|pij|, |pji|) where the signs differ (community.py:48-50)
       const float pij = row[j], pji = col[j];
-      const float mn = min_abs(pij, pji);
-      const bool opp = ((__float_as_uint(pij) ^ __float_as_uint(pji)) >> 31) != 0u;
-      const float ex = opp ? __builtin_copysignf(mn, pij) : 0.0f;
+      const float ex = pair_exchange(pij, pji);
       g = g + (pij - ex);
       pp = pp + ex;
     }
@@ -1775,16 +1773,12 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
 #pragma unroll
     for (int j = 0; j < N; ++j) col[j] = tp[j * 16 + cofs[j & 3]];
     wave_lds_fence();
-    // ex = sign(pij) min(|pij|, |pji|) where the sign bits differ, else +0: one v_min with abs
-    // modifiers (as C++ the compiler canonicalises both operands first), v_bfi for the sign, and
-    // the sign test as an arithmetic-shift mask
+    // ex = sign(pij) min(|pij|, |pji|) where the signs differ (community.py:48-50), one v_med3
     float g = 0.0f, pp = 0.0f;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const float pij = row[j], pji = col[j];
-      const float mn = min_abs(pij, pji);
-      const int opp = (__float_as_int(pij) ^ __float_as_int(pji)) >> 31;
-      const float ex = __int_as_float(__float_as_int(__builtin_copysignf(mn, pij)) & opp);
+      const float ex = pair_exchange(pij, pji);
       g = g + (pij - ex);
       pp = pp + ex;
     }
@@ -1927,9 +1921,7 @@ __global__ __launch_bounds__(kWave) void rule_episode_kernel(const EpisodeParams
     float g = 0.0f, pp = 0.0f;
     for (int j = 0; j < N; ++j) {
       const float pj = shP[sl * G + j];
-      const float mn = min_abs(P, pj);
-      const bool opp = ((__float_as_uint(P) ^ __float_as_uint(pj)) >> 31) != 0u;
-      const float ex = opp ? __builtin_copysignf(mn, P) : 0.0f;
+      const float ex = pair_exchange(P, pj);
       g = g + (P - ex);
       pp = pp + ex;
     }
