@@ -389,6 +389,11 @@ __device__ __forceinline__ float hp_of(const float4& lv, int act) { return sel3(
 __device__ __forceinline__ float pair_exchange(float pij, float pji) {
   return __builtin_amdgcn_fmed3f(pij, -pji, 0.0f);
 }
+// _divide_power's numerator out * |f_j| (agent.py:193) as (-|out|) * f_j: the filter keeps f_j <= 0
+// for out > 0 and f_j >= 0 for out < 0, so f_j = -sign(out) |f_j| and the two products are the same
+// IEEE product up to the sign of a zero (out = 0 or f_j = 0: a zero quotient either way); one
+// hoisted -|out| replaces an |.| per column.
+__device__ __forceinline__ float nabs_out(float out) { return -fabsf(out); }
 
 // ----------------------------------------------------------------- the episode kernel
 // One launch = one episode of T timesteps for every scenario (train_episode / run).
@@ -619,7 +624,7 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
       } else {
         // |f_ii| = 0 (own power is -0): (out * 0) / tot == out * 0 exactly for any non-NaN tot
 #pragma unroll
-        for (int j = 0; j < N; ++j) row[j] = (j == i) ? (tot == tot ? out * 0.0f : tot) : FDIV(out * fabsf(f[j]), tot);
+        for (int j = 0; j < N; ++j) row[j] = (j == i) ? (tot == tot ? out * 0.0f : tot) : FDIV(nabs_out(out) * f[j], tot);
       }
       if (active && (rec & 96u)) {
         const size_t kk = (tA * R1) + (size_t)r * A;
@@ -1306,11 +1311,12 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       // out * |f_j| / tot for every j: the diagonal's f_ii = +-0 gives out * 0 / tot = out * 0, the
       // reference's value for it (agent.py:193-194), for any tot > 0.  One range guard per round.
       const Recip rt = recip(tot == 0.0f ? 1.0f : tot);  // the tot = 0 lanes take ev
+      const float nout = nabs_out(out);
       float num[N];
       bool bad = !rt.ok;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
-        num[j] = out * fabsf(f[j]);
+        num[j] = nout * f[j];
         row[j] = fdiv_core(num[j], rt);
         bad = bad || !fdiv_ok(num[j]);
       }
@@ -1728,9 +1734,10 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
       tot = fabsf(tot);
       const float ev = div_n<N>(out * 1.0f);
       const Recip rt = recip(tot == 0.0f ? 1.0f : tot);
+      const float nout = nabs_out(out);
       float num[N];
 #pragma unroll
-      for (int j = 0; j < N; ++j) num[j] = out * fabsf(f[j]);
+      for (int j = 0; j < N; ++j) num[j] = nout * f[j];
       // One wave-uniform range guard instead of one per quotient: the column holds the group's
       // round-0 values, each vouched for by its own lane (ok_ev0), so with out also in range
       // every numerator is 0 or in [2^-38, 2^38] and the packed Newton quotient is exact.
@@ -1750,8 +1757,12 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
           for (int j = 0; j < N; ++j) row[j] = fdiv_ieee(num[j], rt.b);
         }
       }
+      // tot = 0 (every peer's power on out's side of zero) is rare among 16 peers: one wave-uniform
+      // test instead of 16 selects on every step
+      if (__any(tot == 0.0f)) {
 #pragma unroll
-      for (int j = 0; j < N; ++j) row[j] = (tot == 0.0f) ? ev : row[j];
+        for (int j = 0; j < N; ++j) row[j] = (tot == 0.0f) ? ev : row[j];
+      }
     }
     soc = soc_r;
 
