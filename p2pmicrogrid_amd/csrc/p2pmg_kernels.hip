@@ -104,12 +104,12 @@ __device__ __forceinline__ int argmax3(const Row4<QT>& r) {
   if (r.v[2] > b) { a = 2; }
   return a;
 }
+// max over 3 actions (rl.py:127, np.max): two v_max.  Table entries are never NaN and never -0
+// (tables start at +0 and a TD step q + alpha * d is +0 when q = +0 and d = -0), so the value is
+// the sequential compare's
 template <typename QT>
 __device__ __forceinline__ QT max3(const Row4<QT>& r) {
-  QT b = r.v[0];
-  if (r.v[1] > b) b = r.v[1];
-  if (r.v[2] > b) b = r.v[2];
-  return b;
+  return fmax(fmax(r.v[0], r.v[1]), r.v[2]);
 }
 // QActor.train rl.py:125-129 under NumPy 2: f64 TD arithmetic on double(reward)
 __device__ __forceinline__ double td_update(double qsa, float rw, double qmax, double alpha, double gamma) {
@@ -1103,8 +1103,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const int nbv = k.nb;
   const float km1_T = (float)(k.nT - 1), km2_T = (float)(k.nT - 2), km1_p = (float)(np - 1), kp = (float)np;
   const float mi = active ? p.max_in[a] : 1.0f;
-  const Recip rmi = recip(mi), rmph = recip(k.mph), rmargin = recip(k.margin), rn = recip((float)N);
-  const bool margin_one = p.margin == 1.0f;
+  const Recip rmi = recip(mi), rmph = recip(k.mph), rn = recip((float)N);
   const float4 lv = p.hp_lv[a];
   float tin = active ? p.t_in[a] : k.setpoint;
   float tm = active ? p.t_m[a] : k.setpoint;
@@ -1132,9 +1131,10 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   char* rec_ptr = rec_on ? reinterpret_cast<char*>(recs) + (size_t)a * rec_bytes : rec_dummy;
   const size_t rec_step = rec_on ? A * rec_bytes : 0;
 
-  auto temp_bin = [&](float t_in) {  // idx_temp((T_in - setpoint) / margin) heating.py:118-120, rl.py:93
-    const float dt = t_in - k.setpoint;
-    const float x = margin_one ? dt : fdiv_b(dt, rmargin);
+  // idx_temp((T_in - setpoint) / margin) heating.py:118-120, rl.py:93; the launcher sends this
+  // kernel the reference's margin of 1 only (x / 1 == x exactly), other margins take episode_kernel
+  auto temp_bin = [&](float t_in) {
+    const float x = t_in - k.setpoint;
     return clamp_bin_f(((x + 1.0f) / 2.0f) * km2_T + 1.0f, km1_T);
   };
   auto p2p_bin = [&](float x) { return clamp_bin_f(((x + 1.0f) / 2.0f) * kp, km1_p); };
@@ -1161,7 +1161,8 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const uint32_t c0 = codes_a[0];
   uint32_t c1 = codes_a[(size_t)t1 * A];
   uint32_t c2 = codes_a[(size_t)t2 * A];
-  auto code_of = [&](uint32_t w) { return (TRAIN && active) ? w : 0xFFFFFFFFu; };
+  // masked-off lanes may explore too: they read agent 0's rows and store only to the dummy slots
+  auto code_of = [&](uint32_t w) { return TRAIN ? w : 0xFFFFFFFFu; };
   uint32_t cw = code_of(c0);
   int iT = temp_bin(tin);
   // row arithmetic in 24-bit multiplies (full-rate v_mul_u32_u24; every operand < 2^24)

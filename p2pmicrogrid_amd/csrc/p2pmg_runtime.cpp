@@ -647,7 +647,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
                     c->R + 1 <= 4 && c->mi_ok &&
                     (long long)g.n_time_states * g.n_temp_states * g.n_balance_states < 65536 &&
                     (long long)c->T * c->A < (1LL << 32) && host_div_range(g.minutes_per_hour) &&
-                    host_div_range(g.temp_margin) &&
+                    g.temp_margin == 1.0f &&  // heating.py:90 (the kernel skips the / margin)
                     !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_PHILOX_INKERNEL)) && !env_general;
   // shared table, 16-agent scenarios (configs[2]): episode_sq16_kernel
   const bool sq16 = g.shared_q && c->N == 16 && c->R <= 1 && c->mi_ok && host_div_range(g.minutes_per_hour) &&
