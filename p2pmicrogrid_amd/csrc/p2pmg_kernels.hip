@@ -77,7 +77,8 @@ __device__ __forceinline__ T sel3(int a, T x0, T x1, T x2) {
 }
 // Timing-only ablation builds (scripts/latency_ablation.py): -DP2PMG_ABLATE=1 replaces the
 // episode kernel's Q-row gathers by values derived from the address (no memory access),
-// -DP2PMG_ABLATE=2 replaces f32 divisions by reciprocal multiplies.  Never shipped.
+// -DP2PMG_ABLATE=2 replaces f32 divisions by reciprocal multiplies; in the fast kernel =8 fakes the
+// next step's rows, =9 cuts the TD -> next-step patch dependency, =10 both.  Never shipped.
 #ifndef P2PMG_ABLATE
 #define P2PMG_ABLATE 0
 #endif
@@ -1105,6 +1106,10 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const float mi = active ? p.max_in[a] : 1.0f;
   const Recip rmi = recip(mi), rmph = recip(k.mph), rn = recip((float)N);
   const float4 lv = p.hp_lv[a];
+  // the heat-pump terms of heating.py:44-45 per action: (c_in hp) cop and (c_m hp) cop, the same ops
+  // rc_update applies to the chosen level, hoisted out of the episode
+  const float hin[3] = {(k.c_in * lv.x) * k.cop, (k.c_in * lv.y) * k.cop, (k.c_in * lv.z) * k.cop};
+  const float hm[3] = {(k.c_m * lv.x) * k.cop, (k.c_m * lv.y) * k.cop, (k.c_m * lv.z) * k.cop};
   float tin = active ? p.t_in[a] : k.setpoint;
   float tm = active ? p.t_m[a] : k.setpoint;
   double bcap = 0.0, soc = 0.0;
@@ -1199,6 +1204,22 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     float col[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) { row[j] = 0.0f; col[j] = 0.0f; }
+    // the next step's T_in, temperature bin and table strips for each of the 3 actions
+    // (heating.py:37-56, rl.py:93): they need only this step's state, so they run while the rows
+    // are in flight, and the final action then merely selects one set (issue_next)
+    float tinA[3];
+    uint32_t iTA[3], stA[3], nrA[3];
+    {
+      const float ain = k.inv_ri * (tm - tin) + k.inv_rvent * (e0.t_out - tin);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) {
+        const float d_in = k.inv_ci * (ain + hin[x]);
+        tinA[x] = tin + (d_in * k.spm) * k.slot;
+        iTA[x] = (uint32_t)temp_bin(tinA[x]);
+        stA[x] = strip_of(p1.y & 0xFFFFu, (int)iTA[x]);
+        nrA[x] = strip_of(p1.y >> 16, (int)iTA[x]) + (uint32_t)ip_zero;
+      }
+    }
     row0 = patched(row0, a0, pat);  // the previous step's TD store may have hit a prefetched row
     rowN = patched(rowN, aN, pat);
 
@@ -1216,15 +1237,21 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     int iT1 = 0;
     uint32_t strip1 = 0, cw1 = 0, a0n = 0, aNn = 0;
     Row4<QT> row0n, rowNn, candn[3];
-    auto issue_next = [&](float hp_final) {
-      rc_update(k, e0.t_out, hp_final, tin1, tm1);
-      iT1 = temp_bin(tin1);
-      strip1 = strip_of(p1.y & 0xFFFFu, iT1);
-      const uint32_t nrow1 = strip_of(p1.y >> 16, iT1) + (uint32_t)ip_zero;
+    auto issue_next = [&](int act_final) {
+      const Sel3M m = sel3_masks(act_final);
+      strip1 = __float_as_uint(sel3(m, __uint_as_float(stA[0]), __uint_as_float(stA[1]), __uint_as_float(stA[2])));
+      const uint32_t nrow1 =
+          __float_as_uint(sel3(m, __uint_as_float(nrA[0]), __uint_as_float(nrA[1]), __uint_as_float(nrA[2])));
+      iT1 = (int)__float_as_uint(sel3(m, __uint_as_float(iTA[0]), __uint_as_float(iTA[1]), __uint_as_float(iTA[2])));
+      tin1 = sel3(m, tinA[0], tinA[1], tinA[2]);
+      // HPHeating.step's T_m (heating.py:45,48) for the chosen level, off the gather chain
+      const float d_m = k.inv_cm * (((k.inv_ri * (tin - tm) + k.inv_re * (e0.t_out - tm)) + k.solar) +
+                                    sel3(m, hm[0], hm[1], hm[2]));
+      tm1 = tm + (d_m * k.spm) * k.slot;
       cw1 = code_of(c1);
       a0n = row0_addr(strip1, nrow1, cw1);
       aNn = TRAIN ? nrow1 : a0n;
-#if P2PMG_ABLATE == 8
+#if P2PMG_ABLATE == 8 || P2PMG_ABLATE == 10
       row0n = fake_row(q + a0n * kQPad);
       rowNn = fake_row(q + aNn * kQPad);
 #else
@@ -1236,7 +1263,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         for (int b = 0; b < 3; ++b) candn[b] = gather_row(q + (strip1 + ((ipc1 >> (8 * b)) & 0xFFu)) * kQPad);
       }
     };
-    if constexpr (R1 == 1) issue_next(hp);
+    if constexpr (R1 == 1) issue_next(act);
     float out0 = balw + hp;
     double soc_r = soc;  // tentative SoC of the current round
     if constexpr (BAT) {
@@ -1288,7 +1315,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       acts |= (uint32_t)act << (8 * r);
       ips |= (uint32_t)ip << (8 * r);
       hp = hp_of(lv, act);
-      if (r == R1 - 1) issue_next(hp);
+      if (r == R1 - 1) issue_next(act);
       float out = balw + hp;
       if constexpr (BAT) {
         soc_r = soc;
@@ -1363,7 +1390,11 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
       const QT qnew = td_update(qsa, rw, max3(rowN), k.alpha, k.gamma);
       *(active ? q + srow * kQPad + act : q_dummy) = qnew;
+#if P2PMG_ABLATE == 9 || P2PMG_ABLATE == 10
+      pat = Patch<QT>{0xFFFFFFFFu, 0, (QT)0};  // timing-only: the next step does not wait for this TD
+#else
       pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
+#endif
     }
     if constexpr (narrow) {
       *reinterpret_cast<float2*>(__builtin_assume_aligned(rec_ptr, 8)) = make_float2(rw, cost);
