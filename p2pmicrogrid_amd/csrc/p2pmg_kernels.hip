@@ -1220,8 +1220,11 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         nrA[x] = strip_of(p1.y >> 16, (int)iTA[x]) + (uint32_t)ip_zero;
       }
     }
-    row0 = patched(row0, a0, pat);  // the previous step's TD store may have hit a prefetched row
-    rowN = patched(rowN, aN, pat);
+    // Between the rows' arrival and the next step's gathers the wave issues on the critical path
+    // (the gathers' latency is the rest of the step): only what those addresses need goes there;
+    // the TD target row's patch, T_m, the records and the market wait until the gathers are out.
+    const Patch<QT> pprev = pat;    // the previous step's TD store
+    row0 = patched(row0, a0, pat);  // ... may have hit a prefetched row
 
     // round 0 (P = 0: every filtered power is -0, tot = 0, even split)
     int code = (int)(cw & 0xFF);
@@ -1237,17 +1240,13 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     int iT1 = 0;
     uint32_t strip1 = 0, cw1 = 0, a0n = 0, aNn = 0;
     Row4<QT> row0n, rowNn, candn[3];
+    Sel3M mnext{};
     auto issue_next = [&](int act_final) {
       const Sel3M m = sel3_masks(act_final);
+      mnext = m;
       strip1 = __float_as_uint(sel3(m, __uint_as_float(stA[0]), __uint_as_float(stA[1]), __uint_as_float(stA[2])));
       const uint32_t nrow1 =
           __float_as_uint(sel3(m, __uint_as_float(nrA[0]), __uint_as_float(nrA[1]), __uint_as_float(nrA[2])));
-      iT1 = (int)__float_as_uint(sel3(m, __uint_as_float(iTA[0]), __uint_as_float(iTA[1]), __uint_as_float(iTA[2])));
-      tin1 = sel3(m, tinA[0], tinA[1], tinA[2]);
-      // HPHeating.step's T_m (heating.py:45,48) for the chosen level, off the gather chain
-      const float d_m = k.inv_cm * (((k.inv_ri * (tin - tm) + k.inv_re * (e0.t_out - tm)) + k.solar) +
-                                    sel3(m, hm[0], hm[1], hm[2]));
-      tm1 = tm + (d_m * k.spm) * k.slot;
       cw1 = code_of(c1);
       a0n = row0_addr(strip1, nrow1, cw1);
       aNn = TRAIN ? nrow1 : a0n;
@@ -1263,7 +1262,19 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         for (int b = 0; b < 3; ++b) candn[b] = gather_row(q + (strip1 + ((ipc1 >> (8 * b)) & 0xFFu)) * kQPad);
       }
     };
-    if constexpr (R1 == 1) issue_next(act);
+    // the rest of HPHeating.step for the chosen level, once the gathers are out
+    auto settle_next = [&]() {
+      const Sel3M& m = mnext;
+      iT1 = (int)__float_as_uint(sel3(m, __uint_as_float(iTA[0]), __uint_as_float(iTA[1]), __uint_as_float(iTA[2])));
+      tin1 = sel3(m, tinA[0], tinA[1], tinA[2]);
+      const float d_m = k.inv_cm * (((k.inv_ri * (tin - tm) + k.inv_re * (e0.t_out - tm)) + k.solar) +
+                                    sel3(m, hm[0], hm[1], hm[2]));  // heating.py:45,48
+      tm1 = tm + (d_m * k.spm) * k.slot;
+    };
+    if constexpr (R1 == 1) {
+      issue_next(act);
+      settle_next();
+    }
     float out0 = balw + hp;
     double soc_r = soc;  // tentative SoC of the current round
     if constexpr (BAT) {
@@ -1275,7 +1286,9 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     EnvRow e3;
     uint2 p3;
     uint32_t c3, ipc3 = 0;
-    if constexpr (CAND) {  // no round-1 gather to hide behind: issue the step t + 3 inputs now
+    // the step t + 3 inputs (N = 2: no round-1 gather to hide behind): early, since the unrolled
+    // loop copies them at its back edge, which waits for them
+    if constexpr (CAND) {
       e3 = load_env(envb + eo3);
       p3 = preb[o3];
       c3 = codes_a[o3];
@@ -1315,7 +1328,10 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       acts |= (uint32_t)act << (8 * r);
       ips |= (uint32_t)ip << (8 * r);
       hp = hp_of(lv, act);
-      if (r == R1 - 1) issue_next(act);
+      if (r == R1 - 1) {
+        issue_next(act);
+        settle_next();
+      }
       float out = balw + hp;
       if constexpr (BAT) {
         soc_r = soc;
@@ -1388,7 +1404,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       // QAgent.train agent.py:293-298 -> QActor.train rl.py:119-129
       const uint32_t srow = strip + (uint32_t)ip;
       const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
-      const QT qnew = td_update(qsa, rw, max3(rowN), k.alpha, k.gamma);
+      const QT qnew = td_update(qsa, rw, max3(patched(rowN, aN, pprev)), k.alpha, k.gamma);
       *(active ? q + srow * kQPad + act : q_dummy) = qnew;
 #if P2PMG_ABLATE == 9 || P2PMG_ABLATE == 10
       pat = Patch<QT>{0xFFFFFFFFu, 0, (QT)0};  // timing-only: the next step does not wait for this TD
