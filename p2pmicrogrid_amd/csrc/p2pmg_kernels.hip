@@ -215,6 +215,13 @@ __device__ __forceinline__ float group_sum(float v, int lane, int i, int sl, flo
 struct EnvRow {
   float time, t_out, buy, inj, p2p;
 };
+// {t_out, buy, inj, p2p} of an env row as one 16-B load (the fast kernel's input ring)
+typedef float EnvV __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ EnvV load_envv(const float* e) {
+  EnvV v;
+  __builtin_memcpy(&v, e + 1, sizeof(v));
+  return v;
+}
 __device__ __forceinline__ EnvRow load_env(const float* e) {
   const float4 v = *reinterpret_cast<const float4*>(e);
   return EnvRow{v.x, v.y, v.z, v.w, e[4]};
@@ -1150,30 +1157,28 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const uint32_t* codes_a = p.codes + a;
   const uint32_t* ipc_a = p.pre_ipc + a;  // read only when CAND
   const int t1 = T > 1 ? 1 : 0, t2 = 2 % T;
-  // The per-step inputs (env row, pre-pass word, code word, round-1 bins) are streamed three steps
-  // ahead: loaded at step t for step t + 3.  They are fresh HBM lines every step, and with one
-  // step of distance the mid-step wait for step t + 1's words exposed part of their latency.
+  // The per-step inputs (env row, pre-pass word, code word, round-1 bins) are fresh HBM lines every
+  // step, loaded three steps ahead into a 3-slot ring: slot t % 3 holds step t's, and step t
+  // refills its own slot with step t + 3's once those are dead.  The step loop is unrolled by three,
+  // so every slot is a fixed register set (no copies at the back edge, which would wait for the
+  // loads), and the refills are issued after the step's row gathers: loads complete in issue order,
+  // so a stream load issued ahead of the gathers would hold up the wait for them.
   // Running (uniform, 32-bit) offsets of step t + 3, wrapping at T: T * A < 2^32 on this path.
   const uint32_t TA = (uint32_t)T * (uint32_t)A, env_st = (uint32_t)env_step, env_end = env_st * (uint32_t)T;
   uint32_t o3 = (uint32_t)(3 % T) * (uint32_t)A, eo3 = (uint32_t)(3 % T) * env_st;
 
-  EnvRow e0 = load_env(envb);
-  EnvRow e1 = load_env(envb + (size_t)t1 * env_step);
-  EnvRow e2 = load_env(envb + (size_t)t2 * env_step);
-  uint2 p0 = preb[0];
-  uint2 p1 = preb[(size_t)t1 * A];
-  uint2 p2 = preb[(size_t)t2 * A];
-  const uint32_t c0 = codes_a[0];
-  uint32_t c1 = codes_a[(size_t)t1 * A];
-  uint32_t c2 = codes_a[(size_t)t2 * A];
+  // ring slots as vector values, so each stays one register tuple (a 16-B load's destination)
+  EnvV eS[3] = {load_envv(envb), load_envv(envb + (size_t)t1 * env_step), load_envv(envb + (size_t)t2 * env_step)};
+  uint2 pS[3] = {preb[0], preb[(size_t)t1 * A], preb[(size_t)t2 * A]};
+  uint32_t cS[3] = {codes_a[0], codes_a[(size_t)t1 * A], codes_a[(size_t)t2 * A]};
   // masked-off lanes may explore too: they read agent 0's rows and store only to the dummy slots
   auto code_of = [&](uint32_t w) { return TRAIN ? w : 0xFFFFFFFFu; };
-  uint32_t cw = code_of(c0);
+  uint32_t cw = code_of(cS[0]);
   int iT = temp_bin(tin);
   // row arithmetic in 24-bit multiplies (full-rate v_mul_u32_u24; every operand < 2^24)
   auto strip_of = [&](uint32_t base, int it_) { return __umul24(base + __umul24((uint32_t)it_, (uint32_t)nbv), (uint32_t)np); };
-  uint32_t strip = strip_of(p0.y & 0xFFFFu, iT);
-  uint32_t nrow = strip_of(p0.y >> 16, iT) + (uint32_t)ip_zero;
+  uint32_t strip = strip_of(pS[0].y & 0xFFFFu, iT);
+  uint32_t nrow = strip_of(pS[0].y >> 16, iT) + (uint32_t)ip_zero;
   auto row0_addr = [&](uint32_t st, uint32_t nr, uint32_t c) -> uint32_t {
     const bool need = ((c & 0xFF) == 255) || (TRAIN && R1 == 1);  // greedy, or the TD target itself
     return need ? st + (uint32_t)ip_zero : nr;
@@ -1182,23 +1187,28 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   uint32_t aN = TRAIN ? nrow : a0;
   Row4<QT> row0 = gather_row(q + a0 * kQPad);
   Row4<QT> rowN = gather_row(q + aN * kQPad);
-  uint32_t ipc0 = 0, ipc1 = 0, ipc2 = 0;
+  uint32_t iS[3] = {0u, 0u, 0u};
   Row4<QT> cand[3];
   if constexpr (CAND) {
-    ipc0 = ipc_a[0];
-    ipc1 = ipc_a[(size_t)t1 * A];
-    ipc2 = ipc_a[(size_t)t2 * A];
+    iS[0] = ipc_a[0];
+    iS[1] = ipc_a[(size_t)t1 * A];
+    iS[2] = ipc_a[(size_t)t2 * A];
 #pragma unroll
-    for (int b = 0; b < 3; ++b) cand[b] = gather_row(q + (strip + ((ipc0 >> (8 * b)) & 0xFFu)) * kQPad);
+    for (int b = 0; b < 3; ++b) cand[b] = gather_row(q + (strip + ((iS[0] >> (8 * b)) & 0xFFu)) * kQPad);
   }
   Patch<QT> pat{0xFFFFFFFFu, 0, (QT)0};
   float ep_sum = 0.0f;
   __builtin_amdgcn_s_waitcnt(0);  // enter the loop with nothing in flight (static waits inside)
 
-  // one step; the loop below runs it twice per iteration (a manual unroll: the DPP exchanges are
-  // convergent, so the compiler will not unroll a loop with a runtime trip count), which lets the
-  // register allocator alternate the prefetched rows' registers instead of copying them
-  auto step = [&]() __attribute__((always_inline)) {
+  // one step; the loop below runs it three times per iteration (a manual unroll: the DPP exchanges
+  // are convergent, so the compiler will not unroll a loop with a runtime trip count): the input
+  // ring's slots and the prefetched rows' alternating registers stay put
+  auto step = [&](auto par) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value, P1 = (P + 1) % 3;  // slots of step t and of step t + 1
+    const EnvV ev = eS[P];
+    const EnvRow e0{0.0f, ev.x, ev.y, ev.z, ev.w};
+    const uint2 p0 = pS[P], p1 = pS[P1];
+    const uint32_t c1 = cS[P1], ipc0 = iS[P], ipc1 = iS[P1];
     const float balw = __uint_as_float(p0.x);
     float row[N];
     float col[N];
@@ -1262,6 +1272,11 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         for (int b = 0; b < 3; ++b) candn[b] = gather_row(q + (strip1 + ((ipc1 >> (8 * b)) & 0xFFu)) * kQPad);
       }
     };
+    // step t + 3's code word and round-1 bins into this step's slots (dead since step t - 1 / round 1)
+    auto refill_words = [&]() {
+      cS[P] = codes_a[o3];
+      if constexpr (CAND) iS[P] = ipc_a[o3];
+    };
     // the rest of HPHeating.step for the chosen level, once the gathers are out
     auto settle_next = [&]() {
       const Sel3M& m = mnext;
@@ -1273,6 +1288,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     };
     if constexpr (R1 == 1) {
       issue_next(act);
+      refill_words();
       settle_next();
     }
     float out0 = balw + hp;
@@ -1283,17 +1299,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     const float ev0 = div_n_r<N>(out0 * 1.0f, rn);
 #pragma unroll
     for (int j = 0; j < N; ++j) row[j] = ev0;
-    EnvRow e3;
-    uint2 p3;
-    uint32_t c3, ipc3 = 0;
-    // the step t + 3 inputs (N = 2: no round-1 gather to hide behind): early, since the unrolled
-    // loop copies them at its back edge, which waits for them
-    if constexpr (CAND) {
-      e3 = load_env(envb + eo3);
-      p3 = preb[o3];
-      c3 = codes_a[o3];
-      ipc3 = ipc_a[o3];
-    }
 #pragma unroll
     for (int r = 1; r < R1; ++r) {
       if (r == 1) {
@@ -1319,17 +1324,13 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         rowR = gather_row(q + (need ? strip + (uint32_t)ip : a0) * kQPad);
 #endif
       }
-      if (!CAND && r == R1 - 1) {  // next inputs, issued behind the dependent gather
-        e3 = load_env(envb + eo3);
-        p3 = preb[o3];
-        c3 = codes_a[o3];
-      }
       act = code == 255 ? argmax3(rowR) : code;
       acts |= (uint32_t)act << (8 * r);
       ips |= (uint32_t)ip << (8 * r);
       hp = hp_of(lv, act);
       if (r == R1 - 1) {
         issue_next(act);
+        refill_words();
         settle_next();
       }
       float out = balw + hp;
@@ -1370,11 +1371,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       }
 #pragma unroll
       for (int j = 0; j < N; ++j) row[j] = (tot == 0.0f) ? ev : row[j];
-    }
-    if constexpr (R1 == 1) {
-      e3 = load_env(envb + eo3);
-      p3 = preb[o3];
-      c3 = codes_a[o3];
     }
     soc = soc_r;  // BatteryStorage state after the final round's decision
     pat.row = 0xFFFFFFFFu;  // the next step's rows were issued after the previous TD store
@@ -1421,6 +1417,12 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
     }
     rec_ptr += rec_step;
+    // step t's env row and pre-pass word are dead: step t + 3's into their slots (the barrier keeps
+    // the scheduler from hoisting the loads above the old values' last use, which would need a
+    // second register set and a copy at the loop's back edge)
+    asm volatile("" ::: "memory");
+    eS[P] = load_envv(envb + eo3);
+    pS[P] = preb[o3];
     // avg_reward = sum_t mean_i r (community.py:179), canonical sequential order
     const float m = group_sum<N>(rw, lane, i, sl, nullptr);
     ep_sum = ep_sum + div_n_r<N>(m, rn);
@@ -1428,14 +1430,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     tin = tin1;
     tm = tm1;
     iT = iT1;
-    e0 = e1;
-    e1 = e2;
-    e2 = e3;
-    p0 = p1;
-    p1 = p2;
-    p2 = p3;
-    c1 = c2;
-    c2 = c3;
     o3 += (uint32_t)A;
     o3 = o3 == TA ? 0u : o3;
     eo3 += env_st;
@@ -1447,19 +1441,21 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     row0 = row0n;
     rowN = rowNn;
     if constexpr (CAND) {
-      ipc0 = ipc1;
-      ipc1 = ipc2;
-      ipc2 = ipc3;
 #pragma unroll
       for (int b = 0; b < 3; ++b) cand[b] = candn[b];
     }
   };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
   int t = 0;
-  for (; t + 2 <= T; t += 2) {
-    step();
-    step();
+  for (; t + 3 <= T; t += 3) {
+    step(S0{});
+    step(S1{});
+    step(S2{});
   }
-  if (t < T) step();
+  if (t < T) step(S0{});
+  if (t + 1 < T) step(S1{});
   if (active) {
     if (p.reset_t0)  // agent.reset() at the end of train_episode (community.py:181), fused
       t0_draw(p.seed_lo, p.seed_hi, p.episode + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, tin, tm);
