@@ -1106,7 +1106,18 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const size_t A = (size_t)p.A;
   const KC k = pin_constants(p);
   const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
-  QT* __restrict__ q = reinterpret_cast<QT*>(p.q) + (size_t)a * n_states * kQPad;
+  QT* __restrict__ q = reinterpret_cast<QT*>(p.q) + (size_t)a * n_states * kQPad;  // TD stores
+  // Row gathers as ONE 32-bit offset from the wave's first table (global_load's SGPR-base + VGPR-offset
+  // form: a v_lshl_add_u32 per row instead of a 64-bit address on the act -> gather chain).  The
+  // launcher only sends this kernel tables whose 64-lane span fits 4 GiB.  Masked-off lanes read the
+  // wave's first table.
+  const int a_first = (int)blockIdx.x * spw * N;
+  constexpr uint32_t kRowShift = sizeof(QT) == 8 ? 5 : 4;  // padded row: 32 B (f64) / 16 B (f32)
+  const char* const qwave = reinterpret_cast<const char*>(p.q) + ((size_t)a_first * n_states << kRowShift);
+  const uint32_t qlane = active ? (uint32_t)(a - a_first) * (n_states << kRowShift) : 0u;
+  auto gat = [&](uint32_t row) __attribute__((always_inline)) {
+    return gather_row(reinterpret_cast<const QT*>(qwave + (qlane + (row << kRowShift))));
+  };
   const int np = k.np;
   const int nbv = k.nb;
   const float km1_T = (float)(k.nT - 1), km2_T = (float)(k.nT - 2), km1_p = (float)(np - 1), kp = (float)np;
@@ -1185,8 +1196,8 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   };
   uint32_t a0 = row0_addr(strip, nrow, cw);
   uint32_t aN = TRAIN ? nrow : a0;
-  Row4<QT> row0 = gather_row(q + a0 * kQPad);
-  Row4<QT> rowN = gather_row(q + aN * kQPad);
+  Row4<QT> row0 = gat(a0);
+  Row4<QT> rowN = gat(aN);
   uint32_t iS[3] = {0u, 0u, 0u};
   Row4<QT> cand[3];
   if constexpr (CAND) {
@@ -1194,10 +1205,14 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     iS[1] = ipc_a[(size_t)t1 * A];
     iS[2] = ipc_a[(size_t)t2 * A];
 #pragma unroll
-    for (int b = 0; b < 3; ++b) cand[b] = gather_row(q + (strip + ((iS[0] >> (8 * b)) & 0xFFu)) * kQPad);
+    for (int b = 0; b < 3; ++b) cand[b] = gat((strip + ((iS[0] >> (8 * b)) & 0xFFu)));
   }
   Patch<QT> pat{0xFFFFFFFFu, 0, (QT)0};
   float ep_sum = 0.0f;
+#if P2PMG_TRACE  // timing-only probe: per-step s_memtime splits of one wave, printed at the end
+  uint64_t trW = 0, trC = 0, trR = 0, trLast = 0, trA0 = 0, trWC = 0, trA1 = 0, trMid = 0;
+#define P2PMG_STAMP(v) asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
+#endif
   __builtin_amdgcn_s_waitcnt(0);  // enter the loop with nothing in flight (static waits inside)
 
   // one step; the loop below runs it three times per iteration (a manual unroll: the DPP exchanges
@@ -1234,6 +1249,14 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     // (the gathers' latency is the rest of the step): only what those addresses need goes there;
     // the TD target row's patch, T_m, the records and the market wait until the gathers are out.
     const Patch<QT> pprev = pat;    // the previous step's TD store
+#if P2PMG_TRACE
+    uint64_t tr0, tr1;
+    P2PMG_STAMP(tr0);
+    if (trLast) trR += tr0 - trLast;
+    asm volatile("" ::"v"(row0.v[0]), "v"(row0.v[1]), "v"(row0.v[2]));
+    P2PMG_STAMP(tr1);
+    trW += tr1 - tr0;
+#endif
     row0 = patched(row0, a0, pat);  // ... may have hit a prefetched row
 
     // round 0 (P = 0: every filtered power is -0, tot = 0, even split)
@@ -1264,13 +1287,15 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       row0n = fake_row(q + a0n * kQPad);
       rowNn = fake_row(q + aNn * kQPad);
 #else
-      row0n = gather_row(q + a0n * kQPad);
-      rowNn = gather_row(q + aNn * kQPad);
+      row0n = gat(a0n);  // the rows round 0 and round 1 wait for first, the TD's next-state row last
 #endif
       if constexpr (CAND) {
 #pragma unroll
-        for (int b = 0; b < 3; ++b) candn[b] = gather_row(q + (strip1 + ((ipc1 >> (8 * b)) & 0xFFu)) * kQPad);
+        for (int b = 0; b < 3; ++b) candn[b] = gat((strip1 + ((ipc1 >> (8 * b)) & 0xFFu)));
       }
+#if !(P2PMG_ABLATE == 8 || P2PMG_ABLATE == 10)
+      rowNn = gat(aNn);
+#endif
     };
     // step t + 3's code word and round-1 bins into this step's slots (dead since step t - 1 / round 1)
     auto refill_words = [&]() {
@@ -1310,6 +1335,19 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       if (CAND && r == 1) {
         // the partner's round-0 action picks the prefetched row (its bin is byte b of ipc0)
         const int b = __float_as_int(shfl_xor_c<1>(__int_as_float(act)));
+#if P2PMG_TRACE
+        {
+          uint64_t ta, tb;
+          asm volatile("" ::"v"(b));
+          P2PMG_STAMP(ta);
+          asm volatile("" ::"v"(cand[0].v[0]), "v"(cand[1].v[0]), "v"(cand[2].v[0]), "v"(cand[0].v[2]), "v"(cand[1].v[2]),
+                       "v"(cand[2].v[2]));
+          P2PMG_STAMP(tb);
+          trA0 += ta - tr1;
+          trWC += tb - ta;
+          trMid = tb;
+        }
+#endif
         ip = (int)((ipc0 >> (8 * b)) & 0xFFu);
         rowR = patched(sel_row(b, cand[0], cand[1], cand[2]), strip + (uint32_t)ip, pat);
       } else {
@@ -1321,7 +1359,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
 #if P2PMG_ABLATE == 7
         rowR = fake_row(q + (need ? strip + (uint32_t)ip : a0) * kQPad);
 #else
-        rowR = gather_row(q + (need ? strip + (uint32_t)ip : a0) * kQPad);
+        rowR = gat((need ? strip + (uint32_t)ip : a0));
 #endif
       }
       act = code == 255 ? argmax3(rowR) : code;
@@ -1329,7 +1367,20 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       ips |= (uint32_t)ip << (8 * r);
       hp = hp_of(lv, act);
       if (r == R1 - 1) {
+#if P2PMG_TRACE
+        {
+          uint64_t tc;
+          asm volatile("" ::"v"(act));
+          P2PMG_STAMP(tc);
+          trA1 += tc - trMid;
+          trMid = tc;
+        }
+#endif
         issue_next(act);
+#if P2PMG_TRACE
+        P2PMG_STAMP(trLast);
+        trC += trLast - trMid;
+#endif
         refill_words();
         settle_next();
       }
@@ -1456,6 +1507,12 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   }
   if (t < T) step(S0{});
   if (t + 1 < T) step(S1{});
+#if P2PMG_TRACE
+  if (threadIdx.x == 0 && (blockIdx.x == 0 || (int)blockIdx.x == n_cons / 2 || (int)blockIdx.x == n_cons - 1))
+    printf("TRACE blk %d/%d T %d: per step wait %.1f round0 %.1f waitcand %.1f round1 %.1f issue %.1f rest %.1f\n",
+           (int)blockIdx.x, n_cons, T, (double)trW / T, (double)trA0 / T, (double)trWC / T, (double)trA1 / T,
+           (double)trC / T, (double)trR / (T - 1));
+#endif
   if (active) {
     if (p.reset_t0)  // agent.reset() at the end of train_episode (community.py:181), fused
       t0_draw(p.seed_lo, p.seed_hi, p.episode + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, tin, tm);

@@ -646,6 +646,9 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   const bool fast = !g.shared_q && (!c->battery || c->R + 1 <= p2pmg::kFastBatMaxR1) && c->N <= 8 &&
                     c->R + 1 <= 4 && c->mi_ok &&
                     (long long)g.n_time_states * g.n_temp_states * g.n_balance_states < 65536 &&
+                    // a wave's 64 tables span < 4 GiB (the gathers' 32-bit offsets)
+                    64LL * g.n_time_states * g.n_temp_states * g.n_balance_states * g.n_p2p_states * 4 *
+                            (g.q_dtype == 0 ? 8 : 4) < (1LL << 32) &&
                     (long long)c->T * c->A < (1LL << 32) && host_div_range(g.minutes_per_hour) &&
                     g.temp_margin == 1.0f &&  // heating.py:90 (the kernel skips the / margin)
                     !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_PHILOX_INKERNEL)) && !env_general;
