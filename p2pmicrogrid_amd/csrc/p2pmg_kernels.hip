@@ -1256,6 +1256,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     asm volatile("" ::"v"(row0.v[0]), "v"(row0.v[1]), "v"(row0.v[2]));
     P2PMG_STAMP(tr1);
     trW += tr1 - tr0;
+    trMid = tr1;  // no candidate rows (N != 2 or a battery): "round1" runs from the rows' arrival
 #endif
     row0 = patched(row0, a0, pat);  // ... may have hit a prefetched row
 
