@@ -354,6 +354,30 @@ def issue_roofline(workload: str, kernel_ms: float):
     return out
 
 
+def gather_roofline(n_agents: int, horizon: int, kernel_ms: float):
+    """Dependent-gather floor of the per-agent-table fast kernel: the same geometry (one 5.12 MB
+    f64 table per agent, 32 agents per wave, 5 row gathers per step whose addresses depend on the
+    previous step's rows) with everything else stripped, timed by scripts/ubench_gather.hip
+    (profiles/r02_ubench_gather.jsonl, scripts/gpu_ubench_gather.sh).  frac = that floor over the
+    live kernel time: how much of the episode is the memory round trip the reference's
+    act -> T_in -> next-state dependency forces, and how much is the decision chain on top of it."""
+    path = os.path.join(ROOT, "profiles", "r02_ubench_gather.jsonl")
+    if not os.path.exists(path) or not kernel_ms == kernel_ms:
+        return None
+    for line in open(path):
+        try:
+            d = json.loads(line)
+        except Exception:  # noqa: BLE001
+            continue
+        if (d.get("tables") == n_agents and d.get("steps") == horizon and d.get("rows_per_step") == 5
+                and d.get("agents_per_wave") == 32 and not d.get("pair_lanes") and d.get("pool_rows") == 381):
+            floor_us = d["kernel_us"]
+            return {"unit": "us per launch", "floor": floor_us, "achieved": kernel_ms * 1e3,
+                    "frac": floor_us / (kernel_ms * 1e3), "floor_cycles_per_step": d["cycles_per_step"],
+                    "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def load_traffic(path: str, workload: str):
     """HBM bytes per episode-kernel launch from a committed rocprofv3 PMC summary (or None)."""
     if not path or not os.path.exists(path):
@@ -519,6 +543,10 @@ def main():
         issue = issue_roofline(args.workload, kernel_ms)
         if issue:
             out["roofline"]["issue"] = issue
+        if not (shared or battery or hetero) and q_dtype == "f64" and N == 2 and R == 1:
+            gather = gather_roofline(S * N, T, kernel_ms)
+            if gather:
+                out["roofline"]["gather_floor"] = gather
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args.cpu_seconds, S=(64 if hetero else 256) if N <= 4 else 64,
                               N=N, R=R, T=T, q_dtype=q_dtype, shared=shared, battery=battery,

@@ -1,0 +1,176 @@
+// Dependent row-gather latency in the configs[1] geometry: the memory floor of the fast kernel.
+//
+// episode_fast_kernel runs 8192 agents as 256 waves (one per CU, 32 active lanes); every step each
+// lane gathers 5 rows (32-B padded f64 Q rows, loaded as dwordx4 + dwordx2) of its own 5.12 MB table
+// whose addresses depend on the previous step's rows (act -> T_in bin -> next rows).  This probe
+// keeps exactly that and drops everything else: per step each lane issues RPS gathers whose rows are
+// derived from the data of the previous step's gathers (a short hash), waits for all of them, and
+// folds them in.  So the step time is one dependent round trip of RPS row gathers plus ~15 ALU ops.
+// Each agent draws its rows from a pool of POOL pseudo-random distinct rows of its table (the real
+// kernel touches ~380 distinct rows per agent per episode, ~100 MB over all 8192 tables); launches
+// repeat with the same pools, like the bench's back-to-back episodes, so L2 / MALL warm the same way.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o ubench_gather ubench_gather.hip
+//   ./ubench_gather [tables=8192] [pool=381] [rps=5] [steps=96] [lanes=32] [launches=20] [pair=0]
+// prints one JSON line: kernel us per launch (median of the last half), cycles per step (s_memtime of
+// each wave, averaged), the same with an L1-resident pool of 1 row (the ALU + L1 part of the step).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                             \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                            \
+    }                                                                                     \
+  } while (0)
+
+constexpr uint32_t kStates = 160000;  // 20^4 rows per table
+constexpr uint32_t kRowBytes = 32;    // 4 f64 (3 actions + pad)
+
+__device__ __forceinline__ uint32_t mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__global__ void fill_tables(uint32_t* q, size_t n_words, uint32_t seed) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_words; k += (size_t)gridDim.x * blockDim.x)
+    q[k] = mix((uint32_t)k ^ mix((uint32_t)(k >> 32) + seed));
+}
+
+// pool slot k of agent a -> a row of its table (distinct for k < pool with high probability)
+__device__ __forceinline__ uint32_t pool_row(uint32_t a, uint32_t k) {
+  return (uint32_t)(((uint64_t)mix(k * 0x9E3779B9u + a * 0x85EBCA6Bu + 1u) * kStates) >> 32);
+}
+
+// PAIR: two adjacent lanes per agent, each loading one 16-B half of the row (one dwordx4 per row
+// instead of dwordx4 + dwordx2 per lane); `lanes` then counts agents, 2 * lanes <= 64
+template <int RPS, bool PAIR>
+__global__ __launch_bounds__(64) void chase(const char* __restrict__ q, int lanes, uint32_t pool, int steps,
+                                            uint32_t* __restrict__ sink, unsigned long long* __restrict__ cyc) {
+  const int lane = (int)threadIdx.x;
+  const int ag = PAIR ? lane >> 1 : lane;
+  const bool active = ag < lanes;
+  const uint32_t a = (uint32_t)(blockIdx.x * lanes + (active ? ag : 0));
+  // the kernel's addressing: SGPR base of the wave's first table + a 32-bit lane offset
+  const char* const qwave = q + (size_t)blockIdx.x * lanes * kStates * kRowBytes;
+  const uint32_t qlane = (active ? (uint32_t)ag * kStates * kRowBytes : 0u) + (PAIR ? 16u * (uint32_t)(lane & 1) : 0u);
+  uint32_t h = mix(a + 12345u);
+  uint32_t acc = 0;
+  unsigned long long t0;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int t = 0; t < steps; ++t) {
+    uint4 lo[RPS];
+    uint2 hi[RPS];
+#pragma unroll
+    for (int r = 0; r < RPS; ++r) {
+      const uint32_t k = (uint32_t)(((uint64_t)(h + (uint32_t)r * 97u) * pool) >> 32);
+      const char* p = qwave + (qlane + pool_row(a, k) * kRowBytes);
+      lo[r] = *reinterpret_cast<const uint4*>(p);
+      if (!PAIR) hi[r] = *reinterpret_cast<const uint2*>(p + 16);
+    }
+    uint32_t x = (uint32_t)t;
+#pragma unroll
+    for (int r = 0; r < RPS; ++r) {
+      if (PAIR) {  // both halves in both lanes of the pair (a DPP swap, as an argmax over the row needs)
+        const uint32_t o = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo[r].x, 0xB1, 0xF, 0xF, false);
+        x ^= ((lane & 1) ? o ^ lo[r].y : lo[r].x ^ o);
+      } else {
+        x ^= lo[r].x ^ lo[r].w ^ hi[r].y;
+      }
+    }
+    h = mix(x);
+    acc += h;
+  }
+  unsigned long long t1;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  sink[blockIdx.x * 64 + lane] = acc;
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int RPS, bool PAIR>
+static void run(const char* q, int blocks, int lanes, uint32_t pool, int steps, int launches, uint32_t* sink,
+                unsigned long long* cyc, double& us_med, double& cyc_step) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<double> us;
+  std::vector<unsigned long long> hc(blocks);
+  double cs = 0.0;
+  int nc = 0;
+  for (int l = 0; l < launches; ++l) {
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((chase<RPS, PAIR>), dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.0f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (l >= launches / 2) {
+      us.push_back(ms * 1e3);
+      CK(hipMemcpy(hc.data(), cyc, blocks * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      for (auto c : hc) cs += (double)c / steps;
+      nc += blocks;
+    }
+  }
+  std::sort(us.begin(), us.end());
+  us_med = us[us.size() / 2];
+  cyc_step = cs / nc;
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
+int main(int argc, char** argv) {
+  const int tables = argc > 1 ? atoi(argv[1]) : 8192;
+  const uint32_t pool = argc > 2 ? (uint32_t)atoi(argv[2]) : 381u;
+  const int rps = argc > 3 ? atoi(argv[3]) : 5;
+  const int steps = argc > 4 ? atoi(argv[4]) : 96;
+  const int lanes = argc > 5 ? atoi(argv[5]) : 32;
+  const int launches = argc > 6 ? atoi(argv[6]) : 20;
+  const bool pair = argc > 7 && atoi(argv[7]) != 0;
+  if (tables <= 0 || lanes <= 0 || lanes > (pair ? 32 : 64) || tables % lanes || pool == 0 || steps <= 0 || launches < 2 ||
+      (size_t)lanes * kStates * kRowBytes >= (1ull << 32) || !(rps == 1 || rps == 5)) {
+    fprintf(stderr, "bad arguments\n");
+    return 2;
+  }
+  const int blocks = tables / lanes;
+  const size_t bytes = (size_t)tables * kStates * kRowBytes;
+  char* q = nullptr;
+  uint32_t* sink = nullptr;
+  unsigned long long* cyc = nullptr;
+  CK(hipMalloc(&q, bytes));
+  CK(hipMalloc(&sink, (size_t)blocks * 64 * sizeof(uint32_t)));
+  CK(hipMalloc(&cyc, (size_t)blocks * sizeof(unsigned long long)));
+  hipLaunchKernelGGL(fill_tables, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint32_t*>(q), bytes / 4, 7u);
+  CK(hipDeviceSynchronize());
+  double us = 0, cs = 0, us1 = 0, cs1 = 0;
+  if (rps == 5 && !pair) {
+    run<5, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
+    run<5, false>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
+  } else if (rps == 5) {
+    run<5, true>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
+    run<5, true>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
+  } else if (!pair) {
+    run<1, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
+    run<1, false>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
+  } else {
+    run<1, true>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
+    run<1, true>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
+  }
+  printf("{\"probe\": \"ubench_gather\", \"tables\": %d, \"table_bytes\": %zu, \"pool_rows\": %u, \"rows_per_step\": %d, "
+         "\"steps\": %d, \"agents_per_wave\": %d, \"pair_lanes\": %d, \"waves\": %d, \"launches\": %d, \"kernel_us\": %.2f, "
+         "\"cycles_per_step\": %.1f, \"l1_pool1_kernel_us\": %.2f, \"l1_pool1_cycles_per_step\": %.1f}\n",
+         tables, bytes, pool, rps, steps, lanes, pair ? 1 : 0, blocks, launches, us, cs, us1, cs1);
+  CK(hipFree(q));
+  CK(hipFree(sink));
+  CK(hipFree(cyc));
+  return 0;
+}

@@ -124,6 +124,10 @@ def test_bench_helpers():
     assert bench.epsilon_at(51) == 0.81 * 0.9 * 0.9 and bench.epsilon_at(100000) == 0.1
     assert bench.algorithmic_bytes_per_agent_step(1, 4) == 60  # SURVEY §8(d) 76 B minus the 16 B of state
     assert bench.algorithmic_bytes_per_agent_step(1, 8) == 104
+    # the committed dependent-gather probe matches the configs[1] geometry only
+    g = bench.gather_roofline(8192, 96, 0.080)
+    assert g is not None and 0.0 < g["floor"] < 80.0 and abs(g["frac"] - g["floor"] / 80.0) < 1e-12
+    assert bench.gather_roofline(4096, 96, 0.080) is None and bench.gather_roofline(8192, 672, 0.080) is None
 
 
 def test_device_count_without_gpu_is_zero_or_more():
