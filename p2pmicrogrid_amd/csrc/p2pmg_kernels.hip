@@ -78,7 +78,8 @@ __device__ __forceinline__ T sel3(int a, T x0, T x1, T x2) {
 // Timing-only ablation builds (scripts/latency_ablation.py): -DP2PMG_ABLATE=1 replaces the
 // episode kernel's Q-row gathers by values derived from the address (no memory access),
 // -DP2PMG_ABLATE=2 replaces f32 divisions by reciprocal multiplies; in the fast kernel =8 fakes the
-// next step's rows, =9 cuts the TD -> next-step patch dependency, =10 both.  Never shipped.
+// next step's rows, =9 cuts the TD -> next-step patch dependency, =10 both, =11 drops the final
+// round's divide-power and the market (the cost from the net power alone).  Never shipped.
 #ifndef P2PMG_ABLATE
 #define P2PMG_ABLATE 0
 #endif
@@ -1210,7 +1211,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   Patch<QT> pat{0xFFFFFFFFu, 0, (QT)0};
   float ep_sum = 0.0f;
 #if P2PMG_TRACE  // timing-only probe: per-step s_memtime splits of one wave, printed at the end
-  uint64_t trW = 0, trC = 0, trR = 0, trLast = 0, trA0 = 0, trWC = 0, trA1 = 0, trMid = 0;
+  uint64_t trW = 0, trC = 0, trR = 0, trLast = 0, trA0 = 0, trWC = 0, trA1 = 0, trMid = 0, trCal = 0;
 #define P2PMG_STAMP(v) asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
 #endif
   __builtin_amdgcn_s_waitcnt(0);  // enter the loop with nothing in flight (static waits inside)
@@ -1256,6 +1257,12 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     asm volatile("" ::"v"(row0.v[0]), "v"(row0.v[1]), "v"(row0.v[2]));
     P2PMG_STAMP(tr1);
     trW += tr1 - tr0;
+    {  // calibration: the cost of one stamp (two back to back)
+      uint64_t tcal;
+      P2PMG_STAMP(tcal);
+      trCal += tcal - tr1;
+      tr1 = tcal;
+    }
     trMid = tr1;  // no candidate rows (N != 2 or a battery): "round1" runs from the rows' arrival
 #endif
     row0 = patched(row0, a0, pat);  // ... may have hit a prefetched row
@@ -1390,6 +1397,12 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         soc_r = soc;
         if (bcap > 0.0) out = (float)battery_rule_r((double)out, soc_r, bcap, rcap, bk);
       }
+#if P2PMG_ABLATE == 11  // timing-only: no final-round divide-power and no market (cost from out alone)
+      if (r == R1 - 1) {
+        row[0] = out;
+        continue;
+      }
+#endif
       // _divide_power's filter keeps pw where sign(out) != sign(pw) (agent.py:187-188): for out > 0
       // that is pw <= 0, for out < 0 pw >= 0, for out = 0 any pw.  A kept pw = +-0 and a dropped
       // one (0) are interchangeable: every later use is |f| or a sum that already holds +0.
@@ -1428,8 +1441,11 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     pat.row = 0xFFFFFFFFu;  // the next step's rows were issued after the previous TD store
 
     // CommunityMicrogrid._assign_powers community.py:45-54 on the final P (diagonal kept)
-    exchange<N>(row, col, i, sl, nullptr);
     float g = 0.0f, pp = 0.0f;
+#if P2PMG_ABLATE == 11
+    g = row[0];
+#else
+    exchange<N>(row, col, i, sl, nullptr);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       // ex = sign(pij) * min(|pij|, |pji|) where the signs differ (community.py:48-50)
@@ -1438,6 +1454,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       g = g + (pij - ex);
       pp = pp + ex;
     }
+#endif
     // CommunityMicrogrid._compute_costs community.py:56-65
     float cost = (g >= 0.0f) ? g * e0.buy : g * e0.inj;
     cost = cost + pp * e0.p2p;
@@ -1510,9 +1527,10 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   if (t + 1 < T) step(S1{});
 #if P2PMG_TRACE
   if (threadIdx.x == 0 && (blockIdx.x == 0 || (int)blockIdx.x == n_cons / 2 || (int)blockIdx.x == n_cons - 1))
-    printf("TRACE blk %d/%d T %d: per step wait %.1f round0 %.1f waitcand %.1f round1 %.1f issue %.1f rest %.1f\n",
+    printf("TRACE blk %d/%d T %d: per step wait %.1f round0 %.1f waitcand %.1f round1 %.1f issue %.1f rest %.1f "
+           "(one stamp %.1f)\n",
            (int)blockIdx.x, n_cons, T, (double)trW / T, (double)trA0 / T, (double)trWC / T, (double)trA1 / T,
-           (double)trC / T, (double)trR / (T - 1));
+           (double)trC / T, (double)trR / (T - 1), (double)trCal / T);
 #endif
   if (active) {
     if (p.reset_t0)  // agent.reset() at the end of train_episode (community.py:181), fused
