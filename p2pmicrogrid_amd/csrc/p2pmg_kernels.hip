@@ -1148,7 +1148,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   // vmcnt bookkeeping takes the shortest path through the branch, and the mid-step wait for the
   // round-1 rows then also waits for the previous step's TD store to complete (an HBM write ack).
   constexpr bool narrow = NARROW;
-  static_assert(!(BAT && NARROW), "the battery variant writes FastRec rows");
   const size_t rec_bytes = narrow ? sizeof(float2) : sizeof(FastRec);
   char* const rec_dummy = reinterpret_cast<char*>(reinterpret_cast<FastRec*>(p.dummy) + kWave + lane);
   const bool rec_on = p.record != 0 && active;
@@ -1587,9 +1586,7 @@ void launch_fast_nw(const EpisodeParams& p, const uint2* pre, FastRec* recs, int
 template <int N, typename QT, int R1, bool BAT>
 void launch_fast_b(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
                    const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
-  if constexpr (!BAT) {
-    if (p.rec_narrow) return launch_fast_nw<N, QT, R1, false, true>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
-  }
+  if (p.rec_narrow) return launch_fast_nw<N, QT, R1, BAT, true>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
   launch_fast_nw<N, QT, R1, BAT, false>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
 }
 template <int N, typename QT, int R1>

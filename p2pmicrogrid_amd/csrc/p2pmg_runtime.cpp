@@ -728,8 +728,8 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
       HIP_TRY(c, hipMalloc(&c->rec_pack, (size_t)c->T * c->A * p2pmg::kFastRecBytes));
     p.rec_pack = c->rec_pack;
   }
-  // fast (without battery) / sq16: only {reward, cost} requested -> 8-B record rows
-  p.rec_narrow = ((fast && !p.battery) || sq16) && (args->record & ~(P2PMG_REC_REWARD | P2PMG_REC_COST)) == 0 ? 1 : 0;
+  // fast / sq16: only {reward, cost} requested -> 8-B record rows
+  p.rec_narrow = (fast || sq16) && (args->record & ~(P2PMG_REC_REWARD | P2PMG_REC_COST)) == 0 ? 1 : 0;
   const bool ext = fast || sq16;  // launches that stamp their own timing events
   if (!ext && stamp) HIP_TRY(c, hipEventRecord(r0, c->stream));
   int spw = args->scen_per_wave > 0 ? args->scen_per_wave : env_spw;

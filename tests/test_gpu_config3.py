@@ -87,6 +87,29 @@ def test_shared_battery_hetero_match_oracle(N, R, T, q_dtype, shared, battery, h
     _cmp(ob.run_episode("greedy"), eng.get_records(REC), "greedy")
 
 
+@pytest.mark.parametrize("N", [2, 4])
+def test_battery_fast_kernel_narrow_records_match_oracle(N):
+    """configs[3] shape on the battery fast kernel: only {reward, cost} requested -> 8-B record rows
+    (the bench's request); alternating with full records over back-to-back episodes, every record,
+    the SoC and the tables still equal the oracle's."""
+    S, R, T = 24, 1, 48
+    eng, ob = _setup(S, N, R, T, "f64", False, True, True, seed=21)
+    for e in range(4):
+        narrow = e % 2 == 0
+        rec = ("reward", "cost") if narrow else REC
+        eng.run_episode("train", "philox", episode=e, epsilon=0.6, record=rec)
+        assert eng.last_kernel().startswith("episode_fast_kernel<") and "battery" in eng.last_kernel()
+        out = ob.run_episode("train", rng="philox", episode=e, eps=0.6)
+        got = eng.get_records(rec)
+        if narrow:
+            assert np.array_equal(got["reward"], out["reward"]) and np.array_equal(got["cost"], out["cost"]), e
+        else:
+            _cmp(out, got, ("narrow-alt", N, e))
+        assert np.array_equal(eng.get_soc(), ob.soc), e
+        assert np.array_equal(eng.episode_reward(), out["episode_reward"]), e
+    assert np.array_equal(eng.get_q().reshape(ob.q.shape), ob.q)
+
+
 def test_rccl_allreduce_world1_is_identity():
     from p2pmicrogrid_amd.engine import comm_unique_id
     eng, ob = _setup(16, 16, 1, 12, "f32", True, True, False)
