@@ -35,22 +35,34 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 }
 __device__ __forceinline__ float relu(float x) { return x > 0.0f ? x : 0.0f; }
 
-// butterfly sums: every participating lane ends with the bitwise-same total
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Cross-lane sums as VALU lane moves (DPP and gfx950's v_permlane16/32_swap) instead of
+// ds_bpermute round trips through the LDS unit.  x + swap(x) adds the same two operands in both
+// lanes of every exchanged pair, so each sum below ends bitwise-identical in all its lanes.
+template <int CTRL>
+__device__ __forceinline__ float plus_dpp(float v) {  // v + v[lane per the DPP pattern]
+  return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
-__device__ __forceinline__ float sum16(float v) {  // over the 16 lanes of a row group
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+__device__ __forceinline__ float plus_swap16(float v) {  // rows 0 <-> 1, 2 <-> 3 (lane ^ 16)
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float plus_swap32(float v) {  // halves 0 <-> 1 (lane ^ 32)
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// over the 16 lanes of a row group: lane ^ 1, lane ^ 2 (quad_perm), the other quad of each 8
+// (row_half_mirror), the other 8 of each 16 (row_mirror)
+__device__ __forceinline__ float sum16(float v) {
+  v = plus_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v = plus_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v = plus_dpp<0x141>(v);  // row_half_mirror
+  v = plus_dpp<0x140>(v);  // row_mirror
   return v;
 }
 __device__ __forceinline__ float sum_groups(float v) {  // over the 4 row groups (same lane & 15)
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+  return plus_swap32(plus_swap16(v));
 }
+__device__ __forceinline__ float wave_sum(float v) { return sum_groups(sum16(v)); }
 
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
