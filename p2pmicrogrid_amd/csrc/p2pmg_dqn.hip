@@ -282,7 +282,7 @@ __global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
     const int rj = (int)__umulhi(c0, (uint32_t)(mj + 1));
     idx = rj;
     for (int j = 0; j < kB; ++j) {
-      const int r = __shfl(rj, j, 64);
+      const int r = __builtin_amdgcn_readlane(rj, j);  // lane j's draw (j is uniform: an SGPR read, no LDS trip)
       const bool taken = __ballot(l < j && idx == r) != 0;
       if (l == j) idx = taken ? count - kB + j : r;
     }
