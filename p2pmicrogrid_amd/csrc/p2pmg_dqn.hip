@@ -292,12 +292,17 @@ __global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
 
 // one thread's share of agent a's sampled batch (thread t: sample t / 8, floats t % 8 and, for
 // t % 8 < 2, t % 8 + 8), gathered from the replay ring through the sample kernel's slot indices
-__device__ __forceinline__ void batch_part(const DqnParams& d, int a, int t, float& v0, float& v1) {
-  const int b = t >> 3, k = t & 7;
-  const int slot = reinterpret_cast<const int*>(d.smp)[(size_t)a * kB + b];
+__device__ __forceinline__ int batch_slot(const DqnParams& d, int a, int t) {
+  return reinterpret_cast<const int*>(d.smp)[(size_t)a * kB + (t >> 3)];
+}
+__device__ __forceinline__ void batch_part_at(const DqnParams& d, int a, int t, int slot, float& v0, float& v1) {
+  const int k = t & 7;
   const float* src = d.buf + ((size_t)a * d.cap + (size_t)slot) * kTrans;
   v0 = src[k];
   v1 = k < kTrans - 8 ? src[k + 8] : 0.0f;
+}
+__device__ __forceinline__ void batch_part(const DqnParams& d, int a, int t, float& v0, float& v1) {
+  batch_part_at(d, a, t, batch_slot(d, a, t), v0, v1);
 }
 __device__ __forceinline__ void batch_put(float* dst, int t, float v0, float v1) {
   const int b = t >> 3, k = t & 7;
@@ -330,6 +335,25 @@ __device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const f
   W.b3o = th[kOffB3];
 }
 
+// timing-only probe (-DP2PMG_TRACE): per-phase s_memtime splits of the agent loop, printed for env
+// step 50 by every wave of two workgroups (scripts/dev/gpu_dqn_trace.sh).  A phase's time includes
+// the other workgroup's MFMAs sharing the SIMD, and MFMA results landing after their issue.
+#ifndef P2PMG_TRACE
+#define P2PMG_TRACE 0
+#endif
+#if P2PMG_TRACE
+#define DQN_STAMP(k)                                                             \
+  do {                                                                           \
+    uint64_t t_;                                                                 \
+    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    trp[k] += t_ - tlast;                                                        \
+    tlast = t_;                                                                  \
+  } while (0)
+#else
+#define DQN_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
 template <bool SHARED>
 __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) {  // 2 waves / SIMD
   __shared__ float smpb[2][kB * kTrans];  // this agent's batch and the next one's (prefetched)
@@ -376,8 +400,18 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     if ((size_t)a0 < A) batch_part(d, a0, threadIdx.x, v0, v1);
     batch_put(smpb[0], threadIdx.x, v0, v1);
   }
+  // the next agent's slot index, loaded one agent ahead of its transitions: the dependent pair of
+  // loads never makes the loop wait for a global round trip
+  // (unconditional loads at clamped in-range indices: a branch around them would leave a
+  // loop-carried register copy that waits for every load in flight)
+  const int a_last = (int)A - 1;
+  int slot_n = batch_slot(d, min((int)(blockIdx.x * d.apb) + 1, a_last), threadIdx.x);
   __syncthreads();
 
+#if P2PMG_TRACE
+  uint64_t trp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(tlast)::"memory");
+#endif
   for (int ag = 0; ag < n_ag; ++ag) {
     const int a = d.batch ? 0 : blockIdx.x * d.apb + ag;
     if (!d.batch && a >= (int)A) break;  // block-uniform
@@ -388,8 +422,9 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     float (*smp)[kTrans] = reinterpret_cast<float (*)[kTrans]>(smpb[ag & 1]);
     // prefetch the next agent's batch into registers; it goes to the other buffer at the end
     const bool has_next = !d.batch && ag + 1 < n_ag && a + 1 < (int)A;
-    float nx0 = 0.0f, nx1 = 0.0f;
-    if (has_next) batch_part(d, a + 1, threadIdx.x, nx0, nx1);
+    float nx0, nx1;
+    batch_part_at(d, min(a + 1, a_last), threadIdx.x, (int)min((unsigned)slot_n, (unsigned)(d.cap - 1)), nx0, nx1);
+    slot_n = batch_slot(d, min(a + 2, a_last), threadIdx.x);
 
     // ---- layer 1 (K = 5 padded to 8): Z1 = X W1 + b1, 6 target + 2 online row tiles
     const float bt0 = W.bt0, bo0 = W.bo0, bt1 = W.bt1, bo1 = W.bo1, b1t = W.b1t, b1o = W.b1o;
@@ -417,7 +452,9 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
         if (z > 0.0f) z1mask |= 1u << (4 * rt + r);
       }
     }
+    DQN_STAMP(0);
     __syncthreads();
+    DQN_STAMP(1);
 
     // ---- layer 2 as Z2^T = W2^T H1^T (K = 64): the operands of H1 W2 with the MFMA's A and B
     // swapped, so the accumulator of row tile rt holds data row 16 rt + c16 at the hidden units
@@ -437,6 +474,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       ao[0] = mfma4(bo, H1o[c16][k], ao[0]);
       ao[1] = mfma4(bo, H1o[16 + c16][k], ao[1]);
     }
+    DQN_STAMP(2);
     // ---- layer 3, this wave's 16 units: in-lane over r, then over the 4 row groups (g4)
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt) {
@@ -461,7 +499,9 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       s = sum_groups(s);
       if (g4 == 0) qpart[w][3 * kB + 16 * rt + c16] = s;
     }
+    DQN_STAMP(3);
     __syncthreads();
+    DQN_STAMP(1);
 
     // ---- targets y = r + gamma * max_a' Q_target(ns, a') and dL/dq (rl.py:314-331), for this
     // lane's data rows b = 16 rt + c16
@@ -484,13 +524,17 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       lsum += diff * diff;
       dqsum += dq[rt];
     }
-    if (w == 0) {  // loss = mean (y - q)^2: the 16 lanes of a row group hold the 32 rows
-      const float ls = sum16(lsum), dqs = sum16(dqsum);
+    // the 16 lanes of a row group hold the 32 rows: dL/db3 = sum dq in wave 0, the loss
+    // mean (y - q)^2 (only when it is recorded) in wave 1, so neither holds the others at the barrier
+    if (w == 0) {
+      const float dqs = sum16(dqsum);
+      if (l == 0) gb3 += dqs;
+    } else if (w == 1 && (d.batch || d.rec_loss)) {
+      const float ls = sum16(lsum);
       if (l == 0) {
         const float loss = ls / (float)kB;
         if (d.batch) d.loss_out[0] = loss;
-        else if (d.rec_loss) d.rec_loss[(size_t)d.t * A + a] = loss;
-        gb3 += dqs;
+        else d.rec_loss[(size_t)d.t * A + a] = loss;
       }
     }
 
@@ -507,7 +551,9 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       }
       *reinterpret_cast<float4*>(&dZ2[16 * rt + c16][h0]) = make_float4(dz2[0], dz2[1], dz2[2], dz2[3]);
     }
+    DQN_STAMP(4);
     __syncthreads();
+    DQN_STAMP(1);
     // dW2 = H1^T dZ2 (K = the 32 data rows), accumulator rows = layer-1 units 16 mt + 4 g4 + r,
     // columns = the wave's layer-2 units col
 #pragma unroll
@@ -538,8 +584,17 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       }
     }
     if (has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
+    DQN_STAMP(5);
     __syncthreads();  // every wave is done with this agent's LDS and with the online W2
+    DQN_STAMP(1);
   }
+#if P2PMG_TRACE
+  if (l == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2) && !d.batch && d.t == 50)
+    printf("DQNTRACE blk %d wave %d agents %d, cycles per agent: layer1 %.0f layer2 %.0f layer3 %.0f "
+           "targets+dz2 %.0f backward %.0f barrier waits %.0f\n",
+           (int)blockIdx.x, w, n_ag, (double)trp[0] / n_ag, (double)trp[2] / n_ag, (double)trp[3] / n_ag,
+           (double)trp[4] / n_ag, (double)trp[5] / n_ag, (double)trp[1] / n_ag);
+#endif
 
   gb1 = sum_groups(gb1);
 #pragma unroll
