@@ -315,6 +315,35 @@ def test_narrow_reward_cost_records_match_oracle(N):
     assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
 
 
+@pytest.mark.parametrize("dims,fast", [((40, 40, 40, 40), False), ((30, 20, 20, 30), True)])
+def test_non_default_state_dims_match_oracle(dims, fast):
+    """Other Q-table sizes (agent.py:258-261's 20 x 20 x 20 x 20 as parameters).  The fast kernel
+    addresses a wave's rows as 32-bit offsets from its first table, so it only takes tables whose
+    64-lane span fits 4 GiB (40^4 states x 32 B x 64 does not: the general kernel runs); either way
+    records and tables equal the oracle's."""
+    from oracle.restatement import OracleParams
+    S, N, R, T = 4, 2, 1, 24
+    nt, nT, nb, npp = dims
+    inp = scenario_batch(S, N, T, seed=23)
+    ob = OracleBatch(S=S, N=N, R=R, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in, env_time=inp.time[None],
+                     env_tout=inp.t_out, params=OracleParams(n_time=nt, n_temp=nT, n_bal=nb, n_p2p=npp))
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = DeviceCommunityBatch(S, N, R, T, n_time_states=nt, n_temp_states=nT, n_balance_states=nb,
+                               n_p2p_states=npp)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    for e in range(2):
+        eng.run_episode("train", "philox", episode=e, epsilon=0.5, record=REC)
+        assert eng.last_kernel().startswith("episode_fast_kernel<") == fast, eng.last_kernel()
+        out = ob.run_episode("train", rng="philox", seed=42, episode=e, eps=0.5)
+        _compare(out, eng.get_records(REC), ("dims", dims, e))
+        assert np.array_equal(eng.episode_reward(), out["episode_reward"]), e
+    assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
+    eng.close()
+
+
 def test_timing_period_samples_launches_only():
     """set_timing_period(k): only every k-th episode launch carries timing events; results are
     the same as with every launch timed."""
