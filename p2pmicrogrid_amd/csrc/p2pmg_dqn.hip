@@ -336,7 +336,7 @@ __device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const f
 }
 
 // timing-only probe (-DP2PMG_TRACE): per-phase s_memtime splits of the agent loop, printed for env
-// step 50 by every wave of two workgroups (scripts/dev/gpu_dqn_trace.sh).  A phase's time includes
+// step 50 by every wave of two workgroups (scripts/gpu_dqn_trace.sh).  A phase's time includes
 // the other workgroup's MFMAs sharing the SIMD, and MFMA results landing after their issue.
 #ifndef P2PMG_TRACE
 #define P2PMG_TRACE 0
