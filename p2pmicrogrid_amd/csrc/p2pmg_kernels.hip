@@ -1294,7 +1294,15 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       row0n = fake_row(q + a0n * kQPad);
       rowNn = fake_row(q + aNn * kQPad);
 #else
-      row0n = gat(a0n);  // the rows round 0 and round 1 wait for first, the TD's next-state row last
+      // the rows round 0 and round 1 wait for first, the TD's next-state row last.  Round 0's row
+      // only for the lanes that read it (a greedy round 0, or the TD target at R = 0): an exploring
+      // lane's gather would be address work in the CU's memory pipeline for nothing (an exec-masked
+      // load; configs[1] 79.8 -> 79.0 us, configs[3] 66.2 -> 65.3 ms at the bench's epsilon)
+      {
+        Row4<QT> r0{};
+        if (((cw1 & 0xFF) == 255) || (TRAIN && R1 == 1)) r0 = gat(a0n);
+        row0n = r0;
+      }
 #endif
       if constexpr (CAND) {
 #pragma unroll
