@@ -68,17 +68,102 @@ def epsilon_at(episode: int, eps0: float = 0.81, decay: float = 0.9, every: int 
     return eps
 
 
-def dist_setup():
+def dist_setup(gpus: int):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal only (several ranks on a one-GPU box): every rank on this device
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: launch N ranks with torchrun "
+                         f"--nproc-per-node N, or run bench.py --gpus N without WORLD_SIZE (it spawns them)")
+    # rehearsal only (more ranks than GPUs on one box): the launcher maps rank -> device
     local = int(os.environ.get("P2PMG_BENCH_DEVICE", local))
     if world > 1:
         import torch.distributed as dist  # gloo: barrier + max-time only, no GPU interaction
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     return rank, world, local
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_gpus() -> int:
+    """GPUs this node exposes, counted without initialising HIP in this process: the launcher
+    must stay GPU-free, because its children are the ranks (torch.cuda.device_count() does not
+    initialise the runtime on this image; HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES are honoured
+    by it)."""
+    if os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
+        return 0
+    try:
+        import torch
+        return int(torch.cuda.device_count())
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def launch_ranks(argv, gpus: int) -> int:
+    """``bench.py --gpus N`` without WORLD_SIZE: start N rank processes of this same script (one
+    per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, as torchrun would), wait for all of
+    them, and print rank 0's JSON line with the launcher's facts added.  This process never
+    touches the GPU and never re-execs: the ranks are fresh child processes.  With fewer visible
+    GPUs than ranks (a one-GPU rehearsal) ranks share devices round-robin and the line says so."""
+    import subprocess
+    n_dev = visible_gpus()
+    port = _free_port()
+    procs = []
+    for r in range(gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if 0 < n_dev < gpus:
+            env["P2PMG_BENCH_DEVICE"] = str(r % n_dev)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out0, _ = procs[0].communicate()
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    line = None
+    for ln in (out0 or "").splitlines():
+        ln = ln.strip()
+        if ln.startswith("{"):
+            try:
+                line = json.loads(ln)
+            except ValueError:
+                continue
+        elif ln:
+            print(ln, flush=True)
+    if any(rcs) or line is None:
+        print(f"bench.py launcher: rank exit codes {rcs}", file=sys.stderr, flush=True)
+        return next((rc for rc in rcs if rc), 1)
+    line["launcher"] = {"kind": "bench.py spawn (subprocess per rank)", "ranks": gpus, "rank_exit_codes": rcs,
+                        "visible_gpus": n_dev, "ranks_share_gpus": bool(0 < n_dev < gpus)}
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+def engine_class():
+    """The HIP engine.  P2PMG_BENCH_TEST_ENGINE=module:Class swaps in a host stand-in so the CPU
+    test suite can drive the launcher and the collectives end to end; a line produced that way
+    carries ``test_engine`` and is not a measurement."""
+    spec = os.environ.get("P2PMG_BENCH_TEST_ENGINE")
+    if not spec:
+        from p2pmicrogrid_amd.engine import DeviceCommunityBatch
+        return DeviceCommunityBatch
+    import importlib
+    mod, cls = spec.split(":")
+    return getattr(importlib.import_module(mod), cls)
+
+
+def all_gather_float(x: float, world: int):
+    if world == 1:
+        return [x]
+    import torch
+    import torch.distributed as dist
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(out, torch.tensor([x], dtype=torch.float64))
+    return [float(t.item()) for t in out]
 
 
 def barrier(world):
@@ -96,7 +181,7 @@ def rccl_comm(eng, rank: int, world: int, required: bool = False) -> str:
     from p2pmicrogrid_amd.distributed import broadcast_bytes
     from p2pmicrogrid_amd.engine import comm_unique_id
     uid = None
-    if rank == 0:
+    if rank == 0 and not os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
         try:
             uid = comm_unique_id()
         except Exception:  # noqa: BLE001  (every rank learns it from the empty id)
@@ -123,16 +208,6 @@ def episode_metrics(eng, world: int, comm_err: str):
     local = eng.episode_reward().astype(np.float64)
     tot = all_reduce_sum(np.array([local.sum(), local.size]), world)
     return float(tot[0]), int(tot[1])
-
-
-def max_over_ranks(x: float, world: int) -> float:
-    if world == 1:
-        return x
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
 
 
 BATTERY_J = 10.0 * 3.6e6  # 10 kWh per household battery (config 3; the reference fixes no size)
@@ -219,7 +294,8 @@ def main_dqn(args, rank, world, local, S, N, R, T):
             metrics = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
     eng.sync()
     barrier(world)
-    dt = max_over_ranks(time.perf_counter() - t0, world)
+    rank_times = all_gather_float(time.perf_counter() - t0, world)
+    dt = max(rank_times)
     kms = eng.kernel_times()
     steps_per_episode = S * N * T
     flop = dqn_flop_per_agent_step(R)
@@ -244,6 +320,7 @@ def main_dqn(args, rank, world, local, S, N, R, T):
                          "flop_per_episode": flop * steps_per_episode, "timed_launches": int(len(kms))},
             "mean_episode_reward": metrics[0] / metrics[1],
             "rccl_nranks": eng.comm_nranks() if not comm_err else 0,
+            "rank_times_s": rank_times,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_dqn(args.cpu_seconds, R=R, T=T)
@@ -411,10 +488,14 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary for roofline.traffic (default profiles/pmc_traffic[_<workload>].json)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(sys.argv[1:], args.gpus)
 
-    rank, world, local = dist_setup()
+    rank, world, local = dist_setup(args.gpus)
     from p2pmicrogrid_amd.dataset import apply_asset_mix, asset_mix, scenario_batch
-    from p2pmicrogrid_amd.engine import DeviceCommunityBatch
+    DeviceCommunityBatch = engine_class()
 
     S, N, R, T, q_dtype, shared, battery = WORKLOADS[args.workload]
     hetero = args.workload in HETERO
@@ -475,8 +556,8 @@ def main():
             metrics = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
     eng.sync()
     barrier(world)
-    dt = time.perf_counter() - t0
-    dt = max_over_ranks(dt, world)
+    rank_times = all_gather_float(time.perf_counter() - t0, world)
+    dt = max(rank_times)
     kms = eng.kernel_times()
     ep_reward = metrics[0] / metrics[1]
     nranks = eng.comm_nranks() if not comm_err else 0
@@ -532,7 +613,10 @@ def main():
                          "timed_launches": int(len(kms)), "timing_period": timing_period},
             "mean_episode_reward": ep_reward,
             "rccl_nranks": nranks,
+            "rank_times_s": rank_times,
         }
+        if os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
+            out["test_engine"] = os.environ["P2PMG_BENCH_TEST_ENGINE"]
         if comm_err:
             out["rccl_error"] = comm_err
         if shared:
@@ -564,4 +648,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -375,12 +375,32 @@ def setting_name(nr_agents=None, rounds=None, homogeneous=None) -> str:
     return f'{n}-multi-agent-com-rounds-{r}-{"homo" if h else "hetero"}'
 
 
-def main(load_agents: bool = False, episodes: Optional[int] = None, save: bool = True,
-         verbose: bool = True, con=None) -> Dict[str, Any]:
-    """community.py:248-321 training loop: epsilon decay after episodes 0, 50, ...; the running
-    means go to ``training_progress`` when a connection is given (db.log_training_progress);
-    checkpoints every ``save_episodes`` and at the end.  Plotting is out of scope."""
+def _set_day_profiles(community: CommunityMicrogrid, agent_dfs, rows=None) -> None:
+    """community.py:306-311 / :386-391: each agent's load and PV of the evaluation data, scaled by
+    the homogeneous ratings or by fresh N(0.7, 0.2) / N(4, 0.2) draws (load first, then PV, per
+    agent: the reference's np.random consumption order)."""
+    for i, agent in enumerate(community.agents):
+        df = agent_dfs[i] if rows is None else agent_dfs[i].loc[rows]
+        agent_load = ds.dataframe_to_dataset(df['load'] * (0.7e3 if setup.homogeneous
+                                                           else np.random.normal(0.7, 0.2, 1) * 1e3))
+        agent_pv = ds.dataframe_to_dataset(df['pv'] * (4e3 if setup.homogeneous
+                                                       else np.random.normal(4, 0.2, 1) * 1e3))
+        agent.set_profiles(agent_load, agent_pv)
+
+
+def main(con=None, load_agents: bool = False, analyse: bool = False, *, episodes: Optional[int] = None,
+         save: bool = True, verbose: bool = True) -> Dict[str, Any]:
+    """community.py:248-321 (same positional signature: ``main(db_connection, load_agents=True,
+    analyse=True)`` as at community.py:436).  Episodes ``setup.starting_episodes`` ..
+    ``setup.max_episodes`` (``episodes`` = a shorter run), epsilon decay after episodes 0, 50, ...,
+    running means to ``training_progress`` (db.log_training_progress) when a connection is given,
+    ``.npy`` checkpoints every ``setup.save_episodes`` and at the end.  ``analyse`` runs the
+    reference's greedy validation rollout (community.py:302-316: validation split, fresh rating
+    draws, community.run) and returns its power/cost; the plots of analyse_community_output
+    (data_analysis.py, out of scope) and save_times' ../data JSON are not produced."""
     setting = setting_name()
+    if verbose:
+        print(setting)
     community = get_rl_based_community(setup.nr_agents, homogeneous=setup.homogeneous)
     if load_agents:
         for agent in community.agents:
@@ -414,7 +434,16 @@ def main(load_agents: bool = False, episodes: Optional[int] = None, save: bool =
     if save:
         for agent in community.agents:
             agent.save_to_file(setting, setup.implementation)
-    return {"community": community, "rewards": history, "train_time": time.time() - t0}
+    out: Dict[str, Any] = {"community": community, "rewards": history, "train_time": time.time() - t0}
+    if analyse:  # community.py:302-316
+        env_df, agent_dfs = ds.get_validation_data()
+        env.setup(ds.dataframe_to_dataset(env_df))
+        _set_day_profiles(community, agent_dfs)
+        t_run = time.time()
+        power, cost = community.run()
+        out.update(run_time=time.time() - t_run, power=power, cost=cost,
+                   cost_per_agent=np.sum(cost, axis=0, dtype=np.float32), decisions=community.decisions.copy())
+    return out
 
 
 def save_community_results(con, is_testing: bool, setting: str, day: int, community: CommunityMicrogrid,
@@ -439,10 +468,12 @@ def save_community_results(con, is_testing: bool, setting: str, day: int, commun
                 db.log_rounds_decision(con, setting, a, days, times, r, community.decisions[:, r, a].tolist())
 
 
-def load_and_run(is_testing: bool = False, con=None) -> Dict[int, Dict[str, np.ndarray]]:
-    """community.py:364-412: greedy evaluation per test/validation day from the saved tables, a
-    fresh start each day; rows go to the DB when a connection is given (save_community_results);
-    returns per-day power, cost and decisions."""
+def load_and_run(con=None, is_testing: bool = False, analyse: bool = True) -> Dict[int, Dict[str, np.ndarray]]:
+    """community.py:364-412 (same signature: ``load_and_run(db_connection, is_testing=True,
+    analyse=False)`` as at community.py:437): greedy evaluation per test/validation day from the
+    saved tables, a fresh start each day; rows go to the DB when a connection is given
+    (save_community_results); returns per-day power, cost and decisions.  ``analyse`` would only
+    plot (data_analysis.py, out of scope), so it changes nothing here."""
     setting = setting_name()
     community = get_rl_based_community(setup.nr_agents, homogeneous=setup.homogeneous)
     for agent in community.agents:
@@ -457,12 +488,7 @@ def load_and_run(is_testing: bool = False, con=None) -> Dict[int, Dict[str, np.n
     for day in days:
         env.setup(ds.dataframe_to_dataset(env_df[day_indices[day]]))
         community.reset()
-        for i, agent in enumerate(community.agents):
-            lr = 0.7e3 if setup.homogeneous else np.random.normal(0.7, 0.2, 1) * 1e3
-            agent_load = ds.dataframe_to_dataset(agent_dfs[i].loc[day_indices[day], 'load'] * lr)
-            pr = 4e3 if setup.homogeneous else np.random.normal(4, 0.2, 1) * 1e3
-            agent_pv = ds.dataframe_to_dataset(agent_dfs[i].loc[day_indices[day], 'pv'] * pr)
-            agent.set_profiles(agent_load, agent_pv)
+        _set_day_profiles(community, agent_dfs, day_indices[day])
         power, cost = community.run()
         if con is not None:
             save_community_results(con, is_testing, setting, int(day), community, np.asarray(cost))

@@ -1,0 +1,49 @@
+"""Test-only engine for ``bench.py`` on CPU (P2PMG_BENCH_TEST_ENGINE=bench_test_engine:BenchOracleEngine):
+the oracle-backed OracleEngine behind the DeviceCommunityBatch constructor and the bench's timing /
+communicator calls, so the launcher, sharding and gloo collectives run end to end without a GPU."""
+import numpy as np
+
+from oracle_engine import OracleEngine
+from p2pmicrogrid_amd.distributed import Shard
+
+
+class BenchOracleEngine(OracleEngine):
+    def __init__(self, S, N, R, T, q_dtype="f64", device=0, scenario_offset=0, shared_q=False, seed=42):
+        super().__init__(Shard(0, 1, scenario_offset, S), S, N, R, T, q_dtype, device, seed, shared_q=shared_q)
+        self.device = device
+        self._times = []
+
+    def run_episode(self, mode="train", rng="philox", episode=0, epsilon=0.81, record=(), philox="auto",
+                    next_epsilon=None, reset_sigma=None):
+        super().run_episode(mode, rng, episode=episode, epsilon=epsilon, record=record)
+        if reset_sigma is not None:
+            self.reset_temperatures_philox(episode + 1, reset_sigma)
+        self._times.append(float("nan"))
+
+    def comm_init(self, uid, rank, world):
+        raise RuntimeError("no RCCL in the CPU test engine")
+
+    def sync(self):
+        pass
+
+    def set_timing_period(self, p):
+        pass
+
+    def reset_kernel_times(self):
+        self._times = []
+
+    def kernel_times(self):
+        return np.array([], np.float64)
+
+    def last_kernel(self):
+        return "oracle (CPU test engine)"
+
+    def close(self):
+        pass
+
+    def allreduce_metrics(self):  # world 1 only (comm_init refuses a communicator)
+        r = self.episode_reward().astype(np.float64)
+        return float(r.sum()), int(r.size)
+
+    def comm_nranks(self):
+        return 1

@@ -79,3 +79,47 @@ def test_two_rank_shared_table_exchange_is_world_size_invariant():
     means2, per2, q2 = _run_two_ranks(kw)
     assert np.array_equal(per1, per2) and np.array_equal(q1, q2)
     assert np.allclose(means1, means2, rtol=0, atol=1e-9)
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_2_spawns_two_ranks():
+    """``bench.py --gpus 2`` without torchrun starts 2 rank processes itself (gloo rendezvous on
+    127.0.0.1), shards the scenarios and prints ONE line from rank 0 with n_gpus = 2; the per-rank
+    times and the launcher's record come with it.  The engine is the oracle stand-in."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["P2PMG_BENCH_TEST_ENGINE"] = "bench_test_engine:BenchOracleEngine"
+    env["PYTHONPATH"] = os.pathsep.join([root, os.path.join(root, "tests"), env.get("PYTHONPATH", "")])
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--scenarios", "3", "--horizon", "12", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and len(d["rank_times_s"]) == 2
+    assert d["launcher"]["ranks"] == 2 and d["launcher"]["rank_exit_codes"] == [0, 0]
+    assert d["config"]["agent_steps_per_step"] == 2 * 3 * 2 * 12
+    assert d["test_engine"] and d["rccl_nranks"] == 0 and "rccl_error" in d
+    assert d["ms_per_step"] == pytest.approx(max(d["rank_times_s"]) / 2 * 1e3)
+    # the same episodes in one process (world 1, 6 scenarios) give the same global mean reward
+    cmd1 = [sys.executable, os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1",
+            "--scenarios", "6", "--horizon", "12", "--no-cpu-baseline"]
+    p1 = subprocess.run(cmd1, env=env, capture_output=True, text=True, timeout=240)
+    assert p1.returncode == 0, p1.stderr[-3000:]
+    d1 = json.loads([x for x in p1.stdout.splitlines() if x.startswith("{")][0])
+    assert d1["n_gpus"] == 1
+    assert d1["mean_episode_reward"] == pytest.approx(d["mean_episode_reward"], rel=1e-12)
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE=2" in (p.stderr + p.stdout)

@@ -133,3 +133,42 @@ def test_db_sinks_from_training_and_evaluation(tmp_path, monkeypatch):
             assert np.allclose(rows["heatpump"].values, out[d]["decisions"][:, -1, i])
     rd = db.get_rounds_decisions(con)
     assert len(rd) == 96 * N * len(days) * (setup.rounds + 1)
+
+
+def test_reference_entry_point_calls(tmp_path, monkeypatch):
+    """The reference's own call forms (community.py:436-437), positionally, against a temp
+    SQLite DB: main(db_connection, load_agents=True, analyse=True) resumes from the saved tables,
+    trains, logs and runs the greedy validation rollout; load_and_run(db_connection,
+    is_testing=True, analyse=False) writes test_results and rounds_comparison rows."""
+    from p2pmicrogrid_amd import agent as agent_mod, community, database as db, rl, setup
+    monkeypatch.setattr(rl, "MODELS_DIR", str(tmp_path))
+    monkeypatch.setattr(setup, "max_episodes", 101)  # decays after 0, 50, 100; checkpoints at 50, 100
+    db_connection = db.get_connection(str(tmp_path / "results.db"))
+    db.create_tables(db_connection.cursor())
+    np.random.seed(42)
+    first = community.main(db_connection)  # fresh training, saves the tables
+    saved = [a.actor.q_table.copy() for a in first["community"].agents]
+    loaded = []
+    orig = agent_mod.QAgent.load_from_file
+
+    def spy(self, setting, implementation):
+        orig(self, setting, implementation)
+        loaded.append(self.actor.q_table.copy())
+    monkeypatch.setattr(agent_mod.QAgent, "load_from_file", spy)
+    res = community.main(db_connection, load_agents=True, analyse=True)
+    assert len(loaded) == setup.nr_agents and all(np.array_equal(a, b) for a, b in zip(loaded, saved))
+    assert len(res["rewards"]) == 101 and np.all(np.isfinite(res["rewards"]))
+    val_env, _ = community.ds.get_validation_data()
+    T_val, N = len(val_env), setup.nr_agents
+    assert res["power"].shape == (T_val, N) and res["cost"].shape == (T_val, N)
+    assert np.all(np.isfinite(res["cost"])) and res["decisions"].shape == (T_val, setup.rounds + 1, N)
+    prog = db.get_training_progress(db_connection)
+    assert len(prog) == 2 * 4  # episodes 0, 50, 100 + the final row, per main() call
+    community.load_and_run(db_connection, is_testing=True, analyse=False)
+    res_rows = db.get_test_results(db_connection)
+    test_env, _ = community.ds.get_test_data()
+    n_days = len(np.unique(test_env["day"]))
+    assert len(res_rows) == 96 * N * n_days
+    rd = db.get_rounds_decisions(db_connection)
+    assert len(rd) == 96 * N * n_days * (setup.rounds + 1)
+    assert set(np.unique(rd["decision"])) <= {0.0, 1500.0, 3000.0}
