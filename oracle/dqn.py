@@ -137,7 +137,8 @@ def gradients(theta, s, a, r, ns, target, gamma: float, clip: float = 1.0):
 
 def adam_lr(step: int, dp: DQNParams = DQNParams()) -> np.float32:
     """lr * sqrt(1 - beta2^t) / (1 - beta1^t), t = step (1-based), in float64 -> float32."""
-    return F32(dp.lr * np.sqrt(1.0 - dp.beta2 ** step) / (1.0 - dp.beta1 ** step))
+    t = np.asarray(step, np.float64)
+    return (dp.lr * np.sqrt(1.0 - dp.beta2 ** t) / (1.0 - dp.beta1 ** t)).astype(F32)
 
 
 def adam_step(theta, m, v, grad, step: int, dp: DQNParams = DQNParams()):
@@ -145,6 +146,8 @@ def adam_step(theta, m, v, grad, step: int, dp: DQNParams = DQNParams()):
     g = np.array(grad, dtype=F32, copy=True)
     g[..., 0:320] = np.clip(g[..., 0:320], F32(-dp.clip), F32(dp.clip))
     lr_t = adam_lr(step, dp)
+    if np.ndim(lr_t):  # one Adam iteration count per network (rows of theta)
+        lr_t = np.asarray(lr_t, F32)[:, None]
     m += (g - m) * (F32(1) - F32(dp.beta1))
     v += (g * g - v) * (F32(1) - F32(dp.beta2))
     theta -= (m * lr_t) / (np.sqrt(v) + F32(dp.adam_eps))
@@ -211,7 +214,7 @@ class OracleDQNBatch:
         self.target = self.theta.copy()
         self.m = np.zeros_like(self.theta)
         self.v = np.zeros_like(self.theta)
-        self.step = 0                                            # Adam iterations (shared by all nets)
+        self.step = 0              # Adam iterations: one count for all nets, or an [n_nets] array
         cap = self.dqn.capacity
         self.buf = np.zeros((S, N, cap, 10), F32)                # (s[4], a, r, ns[4]) per slot
         self.added = np.zeros((S, N), np.int64)

@@ -8,6 +8,7 @@ denormals are hipcc's defaults and are relied upon as well.
 """
 from __future__ import annotations
 
+import fcntl
 import os
 import subprocess
 import sys
@@ -43,12 +44,25 @@ KERNEL_PARTS = 9  # p2pmg_kernels.hip is compiled once per part (-DP2PMG_PART=k)
 def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=(), jobs: int = 0) -> str:
     """defines: extra -D flags (timing-only ablation builds go to a different ``out``).
     The translation units (9 parts of p2pmg_kernels.hip, p2pmg_dqn.hip, p2pmg_runtime.cpp) compile
-    in parallel into build/obj/<tag>/, then link into one shared library."""
+    in parallel into build/obj/<tag>/, then link into one shared library.  An exclusive file lock
+    per tag serialises concurrent builders (torchrun ranks, pytest-xdist workers that all find the
+    sources newer): the later ones wait, see a fresh library and return without compiling."""
     if out == LIB and not defines and not force and not needs_build():
         return LIB
     tag = "main" if not defines else "_".join(d.replace("=", "") for d in defines)
     obj_dir = os.path.join(ROOT, "build", "obj", tag)
     os.makedirs(obj_dir, exist_ok=True)
+    with open(os.path.join(ROOT, "build", "obj", f"{tag}.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        try:
+            if out == LIB and not defines and not force and not needs_build():
+                return LIB  # another process built it while this one waited
+            return _build_locked(obj_dir, out, defines, jobs, verbose)
+        finally:
+            fcntl.flock(lock, fcntl.LOCK_UN)
+
+
+def _build_locked(obj_dir: str, out: str, defines, jobs: int, verbose: bool) -> str:
     common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
               "-Wall", "-Wno-unused-function", "-Wno-pass-failed", f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
               *[f"-D{d}" for d in defines]]
@@ -72,11 +86,12 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=(),
             for q, _ in running:
                 q.wait()
             raise subprocess.CalledProcessError(proc.returncode, cmd)
-    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
+    tmp = f"{out}.{os.getpid()}.tmp"
+    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
     if verbose:
         print(" ".join(link), flush=True)
     subprocess.run(link, check=True)
-    os.replace(out + ".tmp", out)
+    os.replace(tmp, out)
     return out
 
 

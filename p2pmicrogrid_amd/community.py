@@ -34,7 +34,12 @@ F32 = np.float32
 class CommunityMicrogrid:
 
     def __init__(self, timeline, agents: List[ActingAgent], rounds: int, q_dtype: Optional[str] = None,
-                 device: Optional[int] = None) -> None:
+                 device: Optional[int] = None, *, battery_rule: bool = False) -> None:
+        """community.py:35-43.  ``battery_rule`` (an extension, off by default): apply the battery
+        rule of RuleAgent._update_storage (agent.py:138-153) to the net power of every agent that
+        carries a BatteryStorage, inside the episode kernel.  The reference never calls that rule
+        from an RL agent (agent.py:200-213), so by default a battery is inert, exactly as there:
+        powers and costs equal the NoStorage run and the SoC stays put."""
         self.timeline = timeline
         self.time_length = len(timeline)
         self.agents = agents
@@ -51,6 +56,12 @@ class CommunityMicrogrid:
             raise ValueError(f"a community needs agents of one learner kind, got {kinds}")
         self._dqn = kinds == {"dqn"}
         self._rule = kinds == {"rule"}
+        self._battery_rule = bool(battery_rule)
+        if self._battery_rule and self._dqn:
+            raise NotImplementedError("the in-kernel battery rule is supported for tabular communities")
+        if self._battery_rule and self._rule:
+            raise NotImplementedError("rule_episode_kernel does not apply the battery rule (the reference's "
+                                      "RuleAgent.take_decision never calls _update_storage, agent.py:114-128)")
 
     # ------------------------------------------------------------ device state
     def _new_dqn_engine(self, T, N):
@@ -119,16 +130,15 @@ class CommunityMicrogrid:
         return [a.storage if isinstance(a.storage, BatteryStorage) else None for a in self.agents]
 
     def _push_storage(self, eng):
-        """Capacities and SoC of the agents' batteries (NoStorage = capacity 0) before a launch;
-        the kernels apply the battery rule (agent.py:138-153) to every round's net power."""
+        """With ``battery_rule``: capacities and SoC of the agents' batteries (NoStorage = capacity
+        0) before a launch; the kernel applies the rule to every round's net power.  Without it
+        nothing is uploaded (the reference's inert battery)."""
         bats = self._batteries()
-        if not any(bats):
+        if not (self._battery_rule and any(bats)):
             if self._uploaded.get("battery"):
                 eng.set_battery(None)
                 self._uploaded["battery"] = False
             return
-        if self._dqn:
-            raise NotImplementedError("batteries are supported for tabular and rule-based communities")
         ref = next(b for b in bats if b is not None).battery
         for b in bats:
             if b is not None and (b.battery.min_soc, b.battery.max_soc, b.battery.efficiency) != \
@@ -139,12 +149,22 @@ class CommunityMicrogrid:
         eng.set_battery(cap, ref.min_soc, ref.max_soc, ref.efficiency, soc0=soc)
         self._uploaded["battery"] = True
 
-    def _pull_storage(self, eng):
+    def _pull_storage(self, eng, T: int):
+        """After a launch.  The reference's inert battery: each BatteryStorage steps T times
+        (storage.py:66-68), so its history holds T entries of its unchanged SoC.  With
+        ``battery_rule``: the device's final SoC; the per-step SoC is not recorded on the device,
+        so the history is left as it was (only the step counter advances)."""
+        bats = [b for b in self._batteries() if b is not None]
         if self._uploaded.get("battery"):
             soc = eng.get_soc()[0]
             for b, x in zip(self._batteries(), soc):
                 if b is not None:
                     b.set_soc(x)
+                    b._time += T
+            return
+        for b in bats:
+            for _ in range(T):
+                b.step()
 
     def _pull_records(self, eng, T):
         act = eng.get_record("action")[:, :, 0, :]  # [T, R+1, N]
@@ -168,7 +188,7 @@ class CommunityMicrogrid:
         codes = self._rng.episode_codes(T, self._rounds, N, eps)
         eng.set_replay_codes(codes)
         eng.run_episode("train", "replay", epsilon=float(eps[0]), record=("reward", "action"))
-        self._pull_storage(eng)
+        self._pull_storage(eng, T)
         self._pull_records(eng, T)
         self.last_rewards = eng.get_record("reward")[:, 0, :]
         avg_reward = float(eng.episode_reward()[0])
@@ -185,7 +205,7 @@ class CommunityMicrogrid:
         self._push_temperatures(eng)
         rec = ("grid", "p2p", "cost", "t_in", "action")
         eng.run_episode("greedy", record=rec)
-        self._pull_storage(eng)
+        self._pull_storage(eng, T)
         r = eng.get_records(rec)
         self._pull_records(eng, T)
         t_in, t_m = eng.get_temperatures()

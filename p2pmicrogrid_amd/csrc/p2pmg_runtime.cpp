@@ -101,7 +101,8 @@ struct p2pmg_ctx {
   float* d_ep_acc = nullptr;  // [S]
   float* rec_loss = nullptr;  // [T][A]
   std::vector<int64_t> d_steps;  // Adam iterations done, per network (agent.py:310: one optimizer per agent)
-  float* d_lr = nullptr;      // [n_nets] per-network step sizes when the counts differ
+  float* d_lr = nullptr;      // [T][n_nets] per-network step sizes of one episode when the counts differ
+  size_t d_lr_cap = 0;        // floats allocated at d_lr
   std::vector<float> h_lr;
   int rec_last_mask = 0;      // records the last episode launch wrote (p2pmg_get_record checks it)
   int64_t d_added_min = 0;    // every ring holds at least this many transitions
@@ -1280,8 +1281,6 @@ int p2pmg_dqn_setup(p2pmg_ctx* c, const p2pmg_dqn_config* cfg) {
   HIP_TRY(c, dmalloc(&c->d_ep_acc, (size_t)c->S));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->d_steps.assign((size_t)c->n_nets, 0);
-  HIP_TRY(c, dmalloc(&c->d_lr, (size_t)c->n_nets));
-  c->h_lr.assign((size_t)c->n_nets, 0.0f);
   c->d_added_min = 0;
   return P2PMG_OK;
 }
@@ -1436,21 +1435,37 @@ static float adam_lr(const p2pmg_dqn_config& q, int64_t step) {
   return (float)(q.lr * std::sqrt(1.0 - std::pow(q.beta2, t)) / (1.0 - std::pow(q.beta1, t)));
 }
 
-static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d) {
+static bool dqn_steps_same(const p2pmg_ctx* c) {
+  for (int64_t st : c->d_steps)
+    if (st != c->d_steps[0]) return false;
+  return true;
+}
+
+// p2pmg_dqn_train_batch advanced some networks on their own, so their Adam step counts differ.
+// Every env step advances every network by one, so an episode's per-network step sizes are known
+// up front: one [T][n_nets] table, uploaded once per episode (not a copy + sync per env step).
+static int dqn_upload_lr_table(p2pmg_ctx* c) {
+  const size_t n = c->d_steps.size(), need = (size_t)c->T * n;
+  if (c->d_lr_cap < need) {
+    dfree(c->d_lr);
+    c->d_lr = nullptr;
+    c->d_lr_cap = 0;
+    HIP_TRY(c, dmalloc(&c->d_lr, need));
+    c->d_lr_cap = need;
+  }
+  c->h_lr.resize(need);
+  for (int t = 0; t < c->T; ++t)
+    for (size_t k = 0; k < n; ++k) c->h_lr[(size_t)t * n + k] = adam_lr(c->dcfg, c->d_steps[k] + 1 + t);
+  HIP_TRY(c, hipMemcpyAsync(c->d_lr, c->h_lr.data(), need * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_lr is rewritten by the next such episode
+  return P2PMG_OK;
+}
+
+static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
   // one env step trains every network once (community.py:158-168)
-  bool same = true;
-  for (auto& st : c->d_steps) {
-    ++st;
-    same = same && st == c->d_steps[0];
-  }
+  for (auto& st : c->d_steps) ++st;
   d.lr_t = adam_lr(c->dcfg, c->d_steps[0]);
-  d.lr_net = nullptr;
-  if (!same) {  // p2pmg_dqn_train_batch advanced some networks on their own: per-network step sizes
-    for (size_t k = 0; k < c->d_steps.size(); ++k) c->h_lr[k] = adam_lr(c->dcfg, c->d_steps[k]);
-    HIP_TRY(c, hipMemcpyAsync(c->d_lr, c->h_lr.data(), c->h_lr.size() * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_lr is rewritten by the next step (rare path)
-    d.lr_net = c->d_lr;
-  }
+  d.lr_net = same ? nullptr : c->d_lr + (size_t)d.t * c->d_steps.size();
   HIP_TRY(c, p2pmg::launch_dqn_sample(d, c->stream));
   if (c->n_nets == 1) {
     HIP_TRY(c, p2pmg::launch_dqn_train(d, c->d_blocks, true, c->stream));
@@ -1495,6 +1510,11 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     c->ring.assign(2 * p2pmg_ctx::kRing, nullptr);
     for (auto& ev : c->ring) HIP_TRY(c, hipEventCreate(&ev));
   }
+  const bool same = mode != P2PMG_MODE_TRAIN || dqn_steps_same(c);
+  if (!same) {
+    rc = dqn_upload_lr_table(c);
+    if (rc != P2PMG_OK) return rc;
+  }
   const int slot = (int)(c->n_timed % p2pmg_ctx::kRing);
   HIP_TRY(c, hipEventRecord(c->ring[2 * slot], c->stream));
   for (int t = 0; t < c->T; ++t) {
@@ -1502,7 +1522,7 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     d.e.mode = mode;
     HIP_TRY(c, p2pmg::launch_dqn_act(d, c->stream));
     if (mode == P2PMG_MODE_TRAIN) {
-      rc = dqn_train_step(c, d);
+      rc = dqn_train_step(c, d, same);
       if (rc != P2PMG_OK) return rc;
     }
   }

@@ -34,6 +34,7 @@ class Battery:
 
 
 class Storage(ElectricalAsset):
+    """storage.py:12-33 (plus ``soc`` / ``capacity``, which the device upload reads)."""
 
     @property
     @abstractmethod
@@ -47,12 +48,30 @@ class Storage(ElectricalAsset):
     @abstractmethod
     def is_full(self) -> bool: ...
 
+    @property
+    @abstractmethod
+    def available_space(self) -> float: ...
+
+    @property
+    @abstractmethod
+    def available_energy(self) -> float: ...
+
+    @abstractmethod
+    def to_soc(self, energy: float) -> float: ...
+
+    @abstractmethod
+    def charge(self, amount: float) -> None: ...
+
+    @abstractmethod
+    def discharge(self, amount: float) -> None: ...
+
 
 class BatteryStorage(Storage):
     """A battery whose state of charge the device updates (see the module docstring)."""
 
     def __init__(self, battery: Battery):
         self.battery = battery
+        self._time = 0
         self._history: List[float] = []
 
     @property
@@ -71,6 +90,27 @@ class BatteryStorage(Storage):
     def is_full(self) -> bool:  # storage.py:41-43
         return self.battery.soc >= self.battery.max_soc
 
+    # The per-call bookkeeping of storage.py:45-64, host-side f64 in the reference's op order, for
+    # callers that step a battery themselves (e.g. a ported RuleAgent._update_storage).
+    @property
+    def available_space(self) -> float:  # storage.py:47-50
+        b = self.battery
+        return max(0.0, b.max_soc - b.soc) * b.capacity / np.sqrt(b.efficiency)
+
+    @property
+    def available_energy(self) -> float:  # storage.py:52-55
+        b = self.battery
+        return max(0.0, b.soc - b.min_soc) * b.capacity * np.sqrt(b.efficiency)
+
+    def to_soc(self, energy: float) -> float:  # storage.py:57-58
+        return energy / self.battery.capacity
+
+    def charge(self, amount: float) -> None:  # storage.py:60-61
+        self.battery.soc += np.sqrt(self.battery.efficiency) * amount
+
+    def discharge(self, amount: float) -> None:  # storage.py:63-64
+        self.battery.soc -= amount / np.sqrt(self.battery.efficiency)
+
     def apply_rule(self, balances: Sequence[float]) -> np.ndarray:
         """RuleAgent._update_storage (agent.py:138-153) over a sequence of net balances (W), on the
         device (p2pmg_battery_seq): returns the balances left after the battery, updates the SoC."""
@@ -81,10 +121,12 @@ class BatteryStorage(Storage):
         b.soc = float(soc[0])
         return out[0]
 
-    def step(self) -> None:
+    def step(self) -> None:  # storage.py:66-68
         self._history.append(self.soc)
+        self._time += 1
 
-    def reset(self) -> None:
+    def reset(self) -> None:  # storage.py:70-73
+        self._time = 0
         self._history = []
         self.battery.soc = RESET_SOC
 
@@ -106,6 +148,21 @@ class NoStorage(Storage):
     @property
     def is_full(self) -> bool:
         return True
+
+    @property
+    def available_space(self) -> float:
+        return 0
+
+    @property
+    def available_energy(self) -> float:
+        return 0
+
+    def to_soc(self, energy: float) -> float:
+        return 0
+
+    def charge(self, amount: float) -> None: ...
+
+    def discharge(self, amount: float) -> None: ...
 
     def apply_rule(self, balances: Sequence[float]) -> np.ndarray:
         return np.asarray(balances, np.float64)

@@ -12,6 +12,8 @@ MagicMock that none of the functions below ever calls — SURVEY.md §8c):
   * ``rl.QActor._get_state_indices``       (rl.py:89-95)        -> qactor_idx.npz
   * ``rl.QActor.select_action/train/...``  (rl.py:100-132)      -> qactor_seq.npz, loop_*.npz
   * ``storage.BatteryStorage``             (storage.py:36-76)   -> battery.npz
+  * ``rl.ActorModel.select_action`` + ``rl.ReplayBuffer.add/sample_batch`` (rl.py:173-244) in the
+    DQN community's call order                              -> dqn_draws.npz
   * ``dataset.get_*_data``/``dataframe_to_dataset`` (dataset.py:39-103, database.py:128-147) on a
     small SQLite file in the reference schema                -> dataset.npz
   * the legacy global ``np.random`` stream in the reference's consumption order (§3.5)
@@ -400,6 +402,94 @@ def make_battery(storage):
                         capacity=bat.capacity, min_soc=0.1, max_soc=0.9, efficiency=0.9, soc0=0.5)
 
 
+# ---------------------------------------------------------------- DQN draws (a20)
+class _ActionsProbe:
+    """Stands in for ActorModel.actions (a TF tensor): records the index each action read uses.
+    random_action reads it with np.random.choice's int (rl.py:184), greedy_action with the (mocked)
+    argmax tensor (rl.py:192), so the recorded key tells the branch and the explored action."""
+    shape = (3,)
+
+    def __init__(self):
+        self.keys = []
+
+    def __getitem__(self, k):
+        self.keys.append(k)
+        return MagicMock()
+
+
+def _sample_tags(rl, buf):
+    """ReplayBuffer.sample_batch (rl.py:225-244) on integer-tagged experiences: the tags of the
+    sampled items, in batch order, as handed to the first tf.stack (rl.py:239)."""
+    rl.tf.stack = MagicMock()
+    buf.sample_batch()
+    return [int(x) for x in rl.tf.stack.call_args_list[0].args[0]]
+
+
+def make_dqn_draws(rl, T: int = 96, R: int = 1, N: int = 2, fill_episodes: int = 5, train_episodes: int = 50,
+                   keep=(0, 1, 48, 49)):
+    """The reference DQN community's draws (community.py:125-182, agent.py:301-342): per (t, round,
+    agent) ActorModel.select_action (Python ``random.random()`` then ``np.random.choice`` when
+    exploring, rl.py:173-184); per agent ReplayBuffer.add then, when training, sample_batch
+    (Python ``random.sample``, rl.py:234-237); 5 fill episodes at epsilon 1, then
+    Trainer.initialize_target's sample per agent (rl.py:272-276), then training episodes with
+    main()'s decay (x0.9 after episodes 0, 50, ..., community.py:279-286).  Experiences are tagged
+    with their add count, so a sampled tag t is deque index t - (added - count).  The buffer passes
+    5000 entries (deque eviction, rl.py:207) in the last kept episodes.  Homogeneous (no T0 draws
+    between episodes).  Plus a short-batch sequence (count < 32, rl.py:234-235)."""
+    import random
+    rl.QNetwork = MagicMock  # the Keras model (TF absent) draws nothing from random / np.random
+    random.seed(42)
+    np.random.seed(42)
+    actors = [rl.ActorModel(1) for _ in range(N)]
+    for a in actors:
+        a.actions = _ActionsProbe()
+    bufs = [rl.ReplayBuffer(5 * 1000, 32) for _ in range(N)]
+    added = [0] * N
+    E = fill_episodes + train_episodes
+    codes = np.full((E, T, R + 1, N), GREEDY, np.uint8)
+    eps_used = np.zeros(E)
+    samples = {e: np.zeros((T, N, 32), np.uint16) for e in keep}
+    init_tags = np.zeros((N, 32), np.uint16)
+    for e in range(E):
+        training = e >= fill_episodes
+        eps_used[e] = actors[0]._epsilon
+        for t in range(T):
+            for r in range(R + 1):
+                for i, a in enumerate(actors):
+                    n0 = len(a.actions.keys)
+                    a.select_action(MagicMock())
+                    assert len(a.actions.keys) == n0 + 1
+                    k = a.actions.keys[-1]
+                    if isinstance(k, (int, np.integer)):
+                        codes[e, t, r, i] = int(k)
+            for i in range(N):
+                bufs[i].add(added[i], 0, 0, 0)
+                added[i] += 1
+                if training:
+                    tags = _sample_tags(rl, bufs[i])
+                    if e - fill_episodes in samples:
+                        samples[e - fill_episodes][t, i] = tags
+        if e == fill_episodes - 1:
+            for i in range(N):
+                init_tags[i] = _sample_tags(rl, bufs[i])
+        if training and (e - fill_episodes) % 50 == 0:
+            for a in actors:
+                a.decay_exploration()
+    assert added[0] > 5000 and bufs[0].count == 5000
+    # short batches: a fresh buffer sampled after every add from 1 to 40 (count < 32 first)
+    random.seed(7)
+    sb = rl.ReplayBuffer(5 * 1000, 32)
+    short = []
+    for k in range(40):
+        sb.add(k, 0, 0, 0)
+        short.append(_sample_tags(rl, sb))
+    short_len = np.array([len(x) for x in short])
+    np.savez_compressed(os.path.join(HERE, "dqn_draws.npz"), T=T, R=R, N=N, fill_episodes=fill_episodes,
+                        train_episodes=train_episodes, keep=np.array(keep), codes=codes, eps=eps_used,
+                        init_tags=init_tags, **{f"sample_tags_{e}": samples[e] for e in keep},
+                        short_tags=np.concatenate(short).astype(np.uint16), short_len=short_len)
+
+
 # ---------------------------------------------------------------- data pipeline (f2)
 DATASET_DAYS = (7, 8, 9, 11, 12, 13, 18, 19, 20, 21)  # 7 and 21 fall outside [start, end) (dataset.py:22-25)
 
@@ -473,11 +563,14 @@ def make_dataset():
 
 def main():
     heating, rl, storage, setup = import_reference()
+    if sys.argv[1:] == ["dqn_draws"]:  # regenerate only this fixture
+        return make_dqn_draws(rl)
     make_dataset()
     assert setup.nr_agents == 2 and setup.rounds == 1 and setup.homogeneous is False
     make_heating(heating)
     make_qactor(rl)
     make_battery(storage)
+    make_dqn_draws(rl)
     # thesis community (setup.py:33-35): N=2, rounds=1, heterogeneous
     make_loop(rl, heating, "loop_thesis_T96", N=2, R=1, homogeneous=False, days=1, episodes=3)
     make_loop(rl, heating, "loop_thesis_T672", N=2, R=1, homogeneous=False, days=7, episodes=2)

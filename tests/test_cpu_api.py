@@ -37,3 +37,31 @@ def test_unbound_qactor_table_management(tmp_path, monkeypatch):
     for _ in range(100):
         a.decay_exploration()
     assert a._epsilon == 0.1
+
+
+def test_battery_storage_interface_matches_reference_sequence():
+    """BatteryStorage's reference bookkeeping (available_space/energy, to_soc, charge, discharge,
+    is_full, step; storage.py:36-76), driven by RuleAgent._update_storage's rule (agent.py:138-153)
+    as a caller porting that rule would, reproduces the reference-generated battery.npz exactly."""
+    from conftest import load_golden
+    from p2pmicrogrid_amd.storage import Battery, BatteryStorage, NoStorage
+    d = load_golden("battery")
+    st = BatteryStorage(Battery(float(d["capacity"]), 5e3, float(d["min_soc"]), float(d["max_soc"]),
+                                float(d["efficiency"]), 0.0))
+    st.reset()
+    assert st.soc == float(d["soc0"]) and st._time == 0
+    for k, b in enumerate(d["bal"]):
+        energy = b * 60 * 15
+        if b > 0 and st.available_energy > 0:
+            x = min(energy, st.available_energy)
+            st.discharge(st.to_soc(x))
+            b -= x / (60 * 15)
+        elif b < 0 and not st.is_full:
+            x = min(-energy, st.available_space)
+            st.charge(st.to_soc(x))
+            b += x / (60 * 15)
+        assert b == d["out_bal"][k] and st.battery.soc == d["soc"][k], k
+        st.step()
+    assert st._time == len(d["bal"]) and st.get_history() == [float(x) for x in d["soc"]]
+    ns = NoStorage()
+    assert ns.is_full and ns.available_space == 0 and ns.available_energy == 0 and ns.to_soc(5.0) == 0

@@ -121,3 +121,69 @@ def test_episode_modes_run_and_learn_something():
     assert ob.step == 96 and not np.array_equal(th0, ob.theta)
     g = ob.run_episode("greedy")
     assert np.array_equal(g["action"], np.argmax(g["q"], axis=-1))
+
+
+def _replay_fixture_draws(draw_fn, d):
+    """Re-draw the fixture's episode sequence with ``draw_fn(py, npr, T, R, N, eps, counts)``:
+    5 fill episodes, Trainer.initialize_target's sample per agent, then training episodes."""
+    import random
+    T, R, N = int(d["T"]), int(d["R"]), int(d["N"])
+    F, E = int(d["fill_episodes"]), int(d["train_episodes"])
+    py, npr = random.Random(42), np.random.RandomState(42)
+    added = np.zeros(N, np.int64)
+    codes, tags, init = [], {}, None
+    for e in range(F + E):
+        training = e >= F
+        counts = np.minimum(added, 5000) if training else None
+        c, smp = draw_fn(py, npr, T, R, N, float(d["eps"][e]), counts)
+        codes.append(np.asarray(c))
+        if training:
+            # deque index j of the step's sample -> tag = added-before-step + 1 - count + j
+            step_added = added[None, :] + np.arange(1, T + 1)[:, None]             # [T, N]
+            first = step_added - np.minimum(step_added, 5000)
+            tags[e - F] = np.asarray(smp, np.int64) + first[..., None]
+        added += T
+        if e == F - 1:
+            init = np.array([py.sample(range(int(min(a, 5000))), 32) for a in added])
+    return np.stack(codes), tags, init
+
+
+@pytest.mark.parametrize("which", ["oracle", "package"])
+def test_dqn_draws_match_reference_actor_and_replay_buffer(which):
+    """Pins a20's exploration + replay stream on the reference's own code: ActorModel.select_action
+    (rl.py:173-184) and ReplayBuffer.add/sample_batch (rl.py:209-244), driven in the DQN community's
+    order with tagged experiences (tests/golden/dqn_draws.npz, make_golden.make_dqn_draws), across
+    the 5000-entry deque eviction.  Both the oracle's reference_dqn_replay and the package's
+    rng.dqn_episode_draws (what CommunityMicrogrid uploads as replay codes / samples) reproduce it."""
+    from conftest import load_golden
+    from p2pmicrogrid_amd import rng
+    d = load_golden("dqn_draws")
+    if which == "oracle":
+        from oracle import dqn as odqn
+        fn = lambda py, npr, T, R, N, eps, counts: odqn.reference_dqn_replay(py, npr, T, R, N, eps, counts=counts)  # noqa: E731
+    else:
+        fn = lambda py, npr, T, R, N, eps, counts: rng.dqn_episode_draws(py, npr, T, R, N, [eps] * N, counts=counts)  # noqa: E731
+    codes, tags, init = _replay_fixture_draws(fn, d)
+    assert np.array_equal(codes, d["codes"])
+    assert np.array_equal(init, d["init_tags"])
+    for e in d["keep"]:
+        assert np.array_equal(tags[int(e)], d[f"sample_tags_{int(e)}"]), e
+    assert tags[int(d["keep"][-1])].max() > 5000  # the kept tail episodes sample past the eviction
+
+
+def test_host_replay_buffer_short_batches_match_reference():
+    """rl.ReplayBuffer standalone (host deque): sampling after each of 40 adds (count < 32 first,
+    rl.py:234-235) returns the reference's items in the reference's order."""
+    import random
+    from conftest import load_golden
+    from p2pmicrogrid_amd.rl import ReplayBuffer
+    d = load_golden("dqn_draws")
+    random.seed(7)
+    b = ReplayBuffer(5000, 32)
+    got = []
+    for k in range(40):
+        b.add(np.float32(k), np.float32(0), np.float32(0), np.float32(0))
+        s, _, _, _ = b.sample_batch()
+        got.append(np.asarray(s).reshape(-1))
+    assert np.array_equal([len(x) for x in got], d["short_len"])
+    assert np.array_equal(np.concatenate(got).astype(np.uint16), d["short_tags"])

@@ -172,3 +172,34 @@ def test_reference_entry_point_calls(tmp_path, monkeypatch):
     rd = db.get_rounds_decisions(db_connection)
     assert len(rd) == 96 * N * n_days * (setup.rounds + 1)
     assert set(np.unique(rd["decision"])) <= {0.0, 1500.0, 3000.0}
+
+
+def test_battery_is_inert_by_default_and_opt_in_rule(monkeypatch):
+    """The reference never runs a battery rule for RL agents (agent.py:200-213): a community whose
+    agents carry BatteryStorage trains and runs exactly like the NoStorage one, the SoC stays at
+    its reset value and BatteryStorage.step fills the history.  battery_rule=True (the extension)
+    changes the flows and moves the SoC."""
+    from p2pmicrogrid_amd.community import CommunityMicrogrid
+    from p2pmicrogrid_amd.storage import Battery, BatteryStorage
+    d = load_golden("loop_thesis_T96")
+    T = int(d["T"])
+    outs = []
+    for variant in ("none", "inert", "rule"):
+        com, env = _community_from_fixture(d)
+        if variant != "none":
+            for a in com.agents:
+                a.storage = BatteryStorage(Battery(10 * 3.6e6, 5e3, 0.1, 0.9, 0.9, 0.5))
+            if variant == "rule":
+                com = CommunityMicrogrid(com.timeline, com.agents, com._rounds, battery_rule=True)
+        r1, _ = com.train_episode()
+        rew = com.last_rewards.copy()
+        for a in com.agents:
+            a.heating.set_state(21.0, 21.0)
+        power, cost = com.run()
+        socs = [a.storage.soc for a in com.agents] if variant != "none" else None
+        hist = [len(a.storage.get_history()) for a in com.agents] if variant != "none" else None
+        outs.append((rew, power, cost, socs, hist))
+    base, inert, rule = outs
+    assert all(np.array_equal(x, y) for x, y in zip(base[:3], inert[:3]))
+    assert inert[3] == [0.5, 0.5] and inert[4] == [T, T]
+    assert not np.array_equal(rule[2], base[2]) and any(s != 0.5 for s in rule[3])

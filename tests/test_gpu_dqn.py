@@ -192,3 +192,77 @@ def test_reference_order_replay_thesis_community():
     _compare_episode(eng, out, "train", 0.9)
     _check_trained(eng, ob, th0)
     eng.close()
+
+
+def test_episode_after_uneven_adam_counts():
+    """p2pmg_dqn_train_batch on one network leaves the per-agent Adam counts uneven ([0, 1]);
+    the next training episode then uses each network's own bias-corrected step size at every env
+    step (one per-episode step-size table on the device) and matches the oracle run with the same
+    per-network counts."""
+    S, N, R, T = 1, 2, 1, 40
+    eng, ob = _pair(S, N, R, T, False)
+    th0 = ob.theta.copy()
+    z = np.zeros((32, 4), np.float32)
+    eng.train_batch(z, np.zeros(32, np.float32), np.zeros(32, np.float32), z, net=1)
+    g, _ = odqn.gradients(ob.theta[1:2], z[None], np.zeros((1, 32), np.float32), np.zeros((1, 32), np.float32),
+                          z[None], ob.target[1:2], 0.95)
+    th1, tg1, m1, v1 = ob.theta[1:2].copy(), ob.target[1:2].copy(), ob.m[1:2].copy(), ob.v[1:2].copy()
+    odqn.adam_step(th1, m1, v1, g, 1)
+    odqn.soft_update(tg1, th1, 0.005)
+    ob.theta[1], ob.target[1], ob.m[1], ob.v[1] = th1[0], tg1[0], m1[0], v1[0]
+    ob.step = np.array([0, 1])
+    assert list(eng.net_steps()) == [0, 1]
+    for ep, (mode, eps) in enumerate((("fill", 1.0), ("train", 0.5), ("train", 0.2))):
+        eng.run_episode(mode, "philox", episode=ep, epsilon=eps, record=("reward", "cost", "grid", "p2p", "t_in",
+                                                                          "action", "loss"))
+        out = ob.run_episode(mode, rng="philox", episode=ep, eps=eps)
+        _compare_episode(eng, out, mode, eps)
+        _reset(eng, ob, ep + 1)
+    assert list(eng.net_steps()) == [2 * T, 2 * T + 1]
+    _check_trained(eng, ob, th0)
+    eng.close()
+
+
+def test_replay_samples_past_eviction_match_reference_fixture():
+    """The reference-pinned sample stream (tests/golden/dqn_draws.npz: ReplayBuffer.sample_batch
+    past the 5000-entry deque eviction, rl.py:207,234-237) drives one replay-mode training episode
+    on a full, wrapped ring: the device equals the oracle, and the host view of the device ring
+    (rl.ReplayBuffer bound to it) returns exactly the reference's sampled experiences."""
+    from conftest import load_golden
+    from p2pmicrogrid_amd.rl import ReplayBuffer
+    d = load_golden("dqn_draws")
+    T, R, N = int(d["T"]), int(d["R"]), int(d["N"])
+    F, e = int(d["fill_episodes"]), int(d["keep"][-1])
+    added0 = (F + e) * T                      # adds before that training episode (> 5000)
+    tags = d[f"sample_tags_{e}"].astype(np.int64)       # [T, N, 32]
+    step_added = added0 + np.arange(1, T + 1)
+    first = step_added - np.minimum(step_added, 5000)
+    idx = (tags - first[:, None, None]).astype(np.uint16)  # deque indices
+    eng, ob = _pair(1, N, R, T, False)
+    th0 = ob.theta.copy()
+    rs = np.random.RandomState(11)
+    ring = np.zeros((N, 5000, 10), np.float32)
+    ring[..., 0:4] = rs.uniform(-1, 1, (N, 5000, 4))
+    ring[..., 4] = odqn.ACTION_VALUES[rs.randint(0, 3, (N, 5000))]
+    ring[..., 5] = rs.uniform(-3, 0, (N, 5000))
+    ring[..., 6:10] = rs.uniform(-1, 1, (N, 5000, 4))
+    eng.set_buffer(ring, np.full(N, added0, np.int32))
+    ob.buf[0] = ring
+    ob.added[:] = added0
+    hb = ReplayBuffer(5000, 32)
+    hb.bind(eng, 0)
+    codes = d["codes"][F + e][:, :, None, :]
+    eng.set_replay_codes(codes)
+    eng.set_samples(idx[:, None])
+    eng.run_episode("train", "replay", epsilon=float(d["eps"][F + e]),
+                    record=("reward", "cost", "grid", "p2p", "t_in", "action", "loss"))
+    out = ob.run_episode("train", codes=codes, samples=idx[:, None], rng="replay")
+    _compare_episode(eng, out, "train", float(d["eps"][F + e]))
+    _check_trained(eng, ob, th0)
+    # after the episode the device ring holds added0 + T entries; the deque view is the last 5000
+    rows = hb._device_rows()
+    buf, added = eng.get_buffer()
+    n = int(added[0])
+    assert n == added0 + T and len(rows) == 5000
+    assert np.array_equal(rows, buf[0][(n - 5000 + np.arange(5000)) % 5000])
+    eng.close()
