@@ -70,6 +70,8 @@ struct p2pmg_ctx {
   float* rec_f32[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // reward, cost, grid, p2p, tin
   uint8_t* rec_action = nullptr;
   int32_t* rec_index = nullptr;
+  void* rec_stage = nullptr;  // fast / sq16 launches: one staging buffer the packed rows unpack into
+  size_t rec_stage_bytes = 0;
   float4* hp_lv = nullptr;     // [A] per-agent heat-pump levels
   float* hp_on = nullptr;      // [A] RuleAgent heat-pump state (lazily allocated, starts off)
   double* soc = nullptr;       // [A]
@@ -342,6 +344,7 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   for (auto& b : c->rec_f32) dfree(b);
   dfree(c->rec_action);
   dfree(c->rec_index);
+  if (c->rec_stage) (void)hipFree(c->rec_stage);
   dfree(c->hp_lv);
   dfree(c->hp_on);
   dfree(c->soc);
@@ -637,9 +640,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   if (train && args->rng != P2PMG_RNG_REPLAY && args->rng != P2PMG_RNG_PHILOX) return fail(c, P2PMG_E_INVALID, "rng");
   if (train && args->rng == P2PMG_RNG_REPLAY && !c->have_codes)
     return fail(c, P2PMG_E_STATE, "run_episode: replay mode needs p2pmg_set_replay_codes");
-  int rc = ensure_records(c, args->record);
-  if (rc != P2PMG_OK) return rc;
-  EpisodeParams p = episode_params(c, args);
+  int rc = P2PMG_OK;
   const p2pmg_config& g = c->cfg;
   // fast per-agent-table path (episode_fast_kernel): automatic whenever it applies
   static const int env_spw = [] { const char* v = getenv("P2PMG_SPW"); return v ? atoi(v) : 0; }();
@@ -659,6 +660,14 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
                     host_div_range(g.temp_margin) && g.n_time_states == 20 && g.n_temp_states == 20 &&
                     g.n_balance_states == 20 && g.n_p2p_states == 20 &&
                     !(args->flags & P2PMG_FLAG_GENERAL_KERNEL) && !env_general;
+  // the general kernel writes unpacked records; fast / sq16 write packed rows (rec_pack) that
+  // p2pmg_get_record unpacks into one staging buffer, so those launches allocate no [T][A] arrays
+  // per record (configs[3] at full size: 35 GB less)
+  if (!fast && !sq16) {
+    rc = ensure_records(c, args->record);
+    if (rc != P2PMG_OK) return rc;
+  }
+  EpisodeParams p = episode_params(c, args);
   const int ps = c->pslot;
   p2pmg::PrepOut next{};
   bool produce = false;
@@ -886,13 +895,23 @@ int p2pmg_get_record(p2pmg_ctx* c, int which, void* host) {
   } else {
     return fail(c, P2PMG_E_INVALID, "get_record: unknown record");
   }
-  if (!src || !(c->rec_last_mask & which))
+  if (!(c->rec_last_mask & which))
     return fail(c, P2PMG_E_STATE, "get_record: the last episode launch did not record this");
-  if (c->rec_fast_mask & which) {  // the last episode ran the fast kernel: unpack its rows
+  if (c->rec_fast_mask & which) {  // the last episode ran the fast / sq16 kernel: unpack its rows
+    if (c->rec_stage_bytes < bytes) {
+      if (c->rec_stage) (void)hipFree(c->rec_stage);
+      c->rec_stage = nullptr;
+      c->rec_stage_bytes = 0;
+      HIP_TRY(c, hipMalloc(&c->rec_stage, bytes));
+      c->rec_stage_bytes = bytes;
+    }
     const int w = slot >= 0 ? slot : (which == P2PMG_REC_ACTION ? 5 : 6);
     const uint32_t tb = (uint32_t)(c->cfg.n_temp_states * c->cfg.n_balance_states);
-    HIP_TRY(c, p2pmg::launch_fast_rec_unpack(c->T, c->R + 1, c->A, tb, c->rec_pack, c->rec_narrow, w, const_cast<void*>(src), c->stream));
+    HIP_TRY(c, p2pmg::launch_fast_rec_unpack(c->T, c->R + 1, c->A, tb, c->rec_pack, c->rec_narrow, w, c->rec_stage,
+                                             c->stream));
+    src = c->rec_stage;
   }
+  if (!src) return fail(c, P2PMG_E_STATE, "get_record: no record buffer");
   HIP_TRY(c, hipMemcpyAsync(host, src, bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return P2PMG_OK;
