@@ -48,6 +48,7 @@ struct EpisodeParams {
   double* soc;               // [A] in/out
   const double* bat_cap;     // [A] capacity in J (0 = no battery)
   double bat_min, bat_max, bat_sqrt_eff;
+  int bat_safe;              // the battery operands lie in battery_rule_r<false>'s verified domain
   const float4* hp_lv;       // [A] per-agent heat-pump power of actions 0..2 (agent.py:268, heating.py:124)
   void* dummy;               // >= 2 * kWave * 32 B scratch: target of the fast kernel's masked-off stores
   uint32_t* pre_ipc;         // fast path, N = 2: [T][A] round-1 p2p bins for the partner's 3 round-0 actions

@@ -1031,6 +1031,12 @@ __device__ __forceinline__ double qcore64(double n, const Recip64& r) {
   const double q = n * r.y;
   return __builtin_copysign(__builtin_fma(__builtin_fma(-r.d, q, n), r.y, q), q);
 }
+// CHECK = false: the launcher has verified the operands' domain (p2pmg_set_battery / set_profiles:
+// capacities 0 or in [2^-20, 2^60], SoC bounds in [2^-100, 2^10], sqrt(eff) in [2^-10, 2^10], SoC0 in
+// [0, 2^10], |load|, |pv|, heat-pump levels <= 2^100).  Then every numerator is 0 or in
+// [2^-252, 2^168] (a positive SoC - bound difference is a multiple of the bound's ulp >= 2^-152; a
+// nonzero f32 balance times 900 lies in [2^-140, 2^138]) and the per-lane range tests go.
+template <bool CHECK = true>
 __device__ __forceinline__ double battery_rule_r(double balance, double& soc, double cap, const Recip64& rcap,
                                                  const BatK& b) {
   const double energy = (balance * 60.0) * 15.0;
@@ -1044,8 +1050,10 @@ __device__ __forceinline__ double battery_rule_r(double balance, double& soc, do
   const double q1 = qcore64(x, rcap);     // x / capacity
   const double q2 = qcore64(x, b.r900);   // x / 900
   const double q3 = qcore64(q1, b.rse);   // (x / capacity) / sqrt(eff)
-  const bool ok = rcap.ok && b.rse.ok && b.r900.ok && q64_ok(x) && q64_ok(q1) && (!chg || q64_ok(space_n));
-  if ((dis || chg) && !ok) return battery_rule(balance, soc, cap, b.smin, b.smax, b.se);  // IEEE divisions
+  if constexpr (CHECK) {
+    const bool ok = rcap.ok && b.rse.ok && b.r900.ok && q64_ok(x) && q64_ok(q1) && (!chg || q64_ok(space_n));
+    if ((dis || chg) && !ok) return battery_rule(balance, soc, cap, b.smin, b.smax, b.se);  // IEEE divisions
+  }
   const double soc_n = dis ? soc - q3 : soc + b.se * q1;
   const double bal_n = dis ? balance - q2 : balance + q2;
   soc = (dis || chg) ? soc_n : soc;
@@ -1692,7 +1700,8 @@ __device__ __forceinline__ pkf2 fdiv_core_pk(pkf2 a, pkf2 b, pkf2 y) {
 #endif
 constexpr int kSq16Waves = 8;                        // waves per workgroup (one hash per 32 scenarios)
 constexpr int kTpStride = 16 * 16 + 16;              // floats per scenario tile (+16: bank offset)
-template <typename QT, int R1, bool TRAIN, bool BAT, bool NARROW>
+// BAT: 0 none, 1 battery with per-lane range tests, 2 battery in the launcher-verified domain
+template <typename QT, int R1, bool TRAIN, int BAT, bool NARROW>
 __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq16_kernel(const EpisodeParams p) {
   constexpr int N = 16, G = 16, SPW = kWave / G;
   __shared__ uint32_t hkey[kSqSlots];
@@ -1732,7 +1741,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   double bcap = 0.0, soc = 0.0;
   BatK bk{};
   Recip64 rcap{};
-  if constexpr (BAT) {
+  if constexpr (BAT != 0) {
     bcap = p.bat_cap[a];
     soc = p.soc[a];
     bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64_u(p.bat_sqrt_eff), recip64_u(900.0)};
@@ -1777,14 +1786,25 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     st.baln = fdiv_b(fn.x - fn.y, rmi);
     const float dt = t_in - k.setpoint;
     const float tnorm = margin_one ? dt : fdiv_b(dt, rmargin);
-    st.it = idx_time(time_t, D.t());
-    st.iT = idx_temp(tnorm, D.T());
-    st.ib = idx_plain(bal, D.b());
-    st.strip = (uint32_t)(((st.it * D.T() + st.iT) * D.b() + st.ib) * D.p());
-    const int itn = idx_time(time_n, D.t());
-    const int ibn = idx_plain(st.baln, D.b());
-    st.nrow = (uint32_t)(((itn * D.T() + st.iT) * D.b() + ibn) * D.p() + ip_zero);
+    // rl.py:89-95 bins of the 20-state axes (the launcher sends this kernel 20^4 tables only), each
+    // as one v_med3 + convert (clamp_bin_f == clamp_bin for every non-NaN value), row offsets in
+    // 24-bit multiplies
+    st.it = clamp_bin_f(time_t * 20.0f, 19.0f);
+    st.iT = clamp_bin_f(((tnorm + 1.0f) / 2.0f) * 18.0f + 1.0f, 19.0f);
+    st.ib = clamp_bin_f(((bal + 1.0f) / 2.0f) * 20.0f, 19.0f);
+    st.strip = __umul24(__umul24(__umul24((uint32_t)st.it, 20u) + (uint32_t)st.iT, 20u) + (uint32_t)st.ib, 20u);
+    const int itn = clamp_bin_f(time_n * 20.0f, 19.0f);
+    const int ibn = clamp_bin_f(((st.baln + 1.0f) / 2.0f) * 20.0f, 19.0f);
+    st.nrow = __umul24(__umul24(__umul24((uint32_t)itn, 20u) + (uint32_t)st.iT, 20u) + (uint32_t)ibn, 20u) +
+              (uint32_t)ip_zero;
     return st;
+  };
+  // the shared table's rows as 32-bit offsets from its (uniform) base: global_load's SGPR-base +
+  // VGPR-offset form instead of a 64-bit address per row (the table spans < 4 GiB)
+  const char* const qb = reinterpret_cast<const char*>(q);
+  constexpr uint32_t kRowShift = sizeof(QT) == 8 ? 5 : 4;
+  auto gatq = [&](uint32_t row) __attribute__((always_inline)) {
+    return gather_row(reinterpret_cast<const QT*>(qb + (row << kRowShift)));
   };
   StepIdx st = step_idx(e0.time, e1.time, fdiv_b(f0.x - f0.y, rmi), f1, tin);
   uint64_t cw = code_word(p, step_codes(p, codes_a, 0, 0, a, W), active);
@@ -1793,8 +1813,8 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     return need ? x.strip + (uint32_t)ip_zero : x.nrow;
   };
   uint32_t a0 = row0_addr(st, cw);
-  Row4<QT> row0 = gather_row(q + a0 * kQPad);
-  Row4<QT> rowN = gather_row(q + (TRAIN ? st.nrow : a0) * kQPad);
+  Row4<QT> row0 = gatq(a0);
+  Row4<QT> rowN = gatq(TRAIN ? st.nrow : a0);
   float ep_sum = 0.0f;
 
   for (int t = 0; t < T; ++t) {
@@ -1814,8 +1834,8 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     uint32_t acts = (uint32_t)act, ips = (uint32_t)ip_zero;
     double soc_r = soc;
     float out = balw + hp;
-    if constexpr (BAT) {
-      if (bcap > 0.0) out = (float)battery_rule_r((double)out, soc_r, bcap, rcap, bk);
+    if constexpr (BAT != 0) {
+      if (bcap > 0.0) out = (float)battery_rule_r<BAT == 1>((double)out, soc_r, bcap, rcap, bk);
     }
     const float ev0 = div_n<N>(out * 1.0f);
     const bool ok_ev0 = in_range19(ev0);
@@ -1835,18 +1855,18 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
       float acc = 0.0f;
 #pragma unroll
       for (int j = 0; j < N; ++j) acc = acc + (-col[j]);
-      ip = idx_plain(fdiv_b(div_n<N>(acc), rmi), D.p());
+      ip = clamp_bin_f(((fdiv_b(div_n<N>(acc), rmi) + 1.0f) / 2.0f) * 20.0f, 19.0f);
       code = (int)((cw >> 8) & 0xFF);
       const bool need = code == 255 || TRAIN;
-      rowR = gather_row(q + (need ? st.strip + (uint32_t)ip : a0) * kQPad);
+      rowR = gatq(need ? st.strip + (uint32_t)ip : a0);
       act = code == 255 ? argmax3(rowR) : code;
       acts |= (uint32_t)act << 8;
       ips |= (uint32_t)ip << 8;
       hp = hp_of(lv, act);
       out = balw + hp;
       soc_r = soc;
-      if constexpr (BAT) {
-        if (bcap > 0.0) out = (float)battery_rule_r((double)out, soc_r, bcap, rcap, bk);
+      if constexpr (BAT != 0) {
+        if (bcap > 0.0) out = (float)battery_rule_r<BAT == 1>((double)out, soc_r, bcap, rcap, bk);
       }
       const float flo = out < 0.0f ? 0.0f : -__builtin_inff(), fhi = out > 0.0f ? 0.0f : __builtin_inff();
       float f[N];
@@ -1897,8 +1917,8 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     const StepIdx st1 = step_idx(e1.time, e2.time, st.baln, f2, tin1);
     const uint64_t cw1 = code_word(p, cw1r, active);
     const uint32_t a0n = row0_addr(st1, cw1);
-    const Row4<QT> row0n = gather_row(q + a0n * kQPad);
-    const Row4<QT> rowNn = gather_row(q + (TRAIN ? st1.nrow : a0n) * kQPad);
+    const Row4<QT> row0n = gatq(a0n);
+    const Row4<QT> rowNn = gatq(TRAIN ? st1.nrow : a0n);
 
     // the final P's column through the swizzled tile (community.py:45-54 needs P[j][i])
 #pragma unroll
@@ -1985,7 +2005,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
       t0_draw(p.seed_lo, p.seed_hi, p.episode + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, tin, tm);
     p.t_in[a] = tin;
     p.t_m[a] = tm;
-    if constexpr (BAT) p.soc[a] = soc;
+    if constexpr (BAT != 0) p.soc[a] = soc;
     if (i == 0) p.ep_reward[s] = ep_sum;
   }
 }
@@ -1993,12 +2013,15 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
 template <typename QT, int R1, bool NARROW>
 void launch_sq16_nw(const EpisodeParams& p, int blocks, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
   const dim3 g(blocks), b(kWave * kSq16Waves);
+  const int bat = !p.battery ? 0 : (p.bat_safe ? 2 : 1);
   if (p.mode == 0) {
-    if (p.battery) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, true, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
-    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, false, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
+    if (bat == 2) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, 2, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
+    else if (bat == 1) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, 1, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
+    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, true, 0, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
   } else {
-    if (p.battery) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, true, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
-    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, false, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
+    if (bat == 2) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, 2, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
+    else if (bat == 1) hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, 1, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
+    else hipExtLaunchKernelGGL((episode_sq16_kernel<QT, R1, false, 0, NARROW>), g, b, 0, st, ev0, ev1, 0, p);
   }
 }
 template <typename QT, int R1>

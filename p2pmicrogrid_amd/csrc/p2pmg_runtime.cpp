@@ -77,6 +77,10 @@ struct p2pmg_ctx {
   double* soc = nullptr;       // [A]
   double* bat_cap = nullptr;   // [A]
   bool battery = false;
+  // operand domains of the battery rule's range-test-free variant (battery_rule_r<false>):
+  bool bat_domain = false;   // capacities, SoC bounds, sqrt(eff) and SoC0 in range (set_battery)
+  bool prof_bounded = false; // every |load|, |pv| <= 2^100 and finite (set_profiles)
+  bool hp_bounded = true;    // every heat-pump level |x| <= 2^100 and finite (defaults: 0 .. 3 kW)
   double bat_min = 0.1, bat_max = 0.9, bat_sqrt_eff = 1.0;
   long long* qdelta = nullptr; // shared table deltas [kDeltaCopies][n_states][4]
   void* comm = nullptr;        // ncclComm_t
@@ -432,6 +436,11 @@ int p2pmg_set_profiles(p2pmg_ctx* c, const float* load_w, const float* pv_w) {
     dfree(dl);
     return fail(c, P2PMG_E_NOMEM, "profile staging");
   }
+  {  // the battery rule's range-test-free variant needs bounded, finite balances (p2pmg_kernels.hip)
+    bool ok = true;
+    for (size_t k = 0; k < n; ++k) ok &= (std::fabs(load_w[k]) <= 0x1p100f) & (std::fabs(pv_w[k]) <= 0x1p100f);
+    c->prof_bounded = ok;
+  }
   e = hipMemcpyAsync(dl, load_w, n * 4, hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(dp, pv_w, n * 4, hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = p2pmg::launch_prof_pack(c->A, c->T, dl, dp, c->prof, c->stream);
@@ -587,6 +596,7 @@ static EpisodeParams episode_params(p2pmg_ctx* c, const p2pmg_episode_args* args
   p.shared_q = g.shared_q ? 1 : 0;
   p.qdelta = c->qdelta;
   p.battery = c->battery ? 1 : 0;
+  p.bat_safe = (c->battery && c->bat_domain && c->prof_bounded && c->hp_bounded) ? 1 : 0;
   p.soc = c->soc;
   p.bat_cap = c->bat_cap;
   p.bat_min = c->bat_min;
@@ -1008,7 +1018,12 @@ int p2pmg_set_hp_levels(p2pmg_ctx* c, const float* levels) {
   if (c) c->inputs_version++;  // invalidates the speculative pre-pass slots
   if (!c || !levels) return P2PMG_E_INVALID;
   std::vector<float4> lv((size_t)c->A);
-  for (size_t a = 0; a < lv.size(); ++a) lv[a] = make_float4(levels[3 * a], levels[3 * a + 1], levels[3 * a + 2], 0.0f);
+  bool ok = true;
+  for (size_t a = 0; a < lv.size(); ++a) {
+    lv[a] = make_float4(levels[3 * a], levels[3 * a + 1], levels[3 * a + 2], 0.0f);
+    for (int k = 0; k < 3; ++k) ok &= std::fabs(levels[3 * a + k]) <= 0x1p100f;
+  }
+  c->hp_bounded = ok;
   HIP_TRY(c, hipMemcpyAsync(c->hp_lv, lv.data(), lv.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return P2PMG_OK;
@@ -1029,6 +1044,16 @@ int p2pmg_set_battery(p2pmg_ctx* c, const double* capacity, double min_soc, doub
   std::vector<double> s0(A, 0.5);
   HIP_TRY(c, hipMemcpyAsync(c->soc, soc0 ? soc0 : s0.data(), A * 8, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  {  // battery_rule_r<false>'s domain (see its comment in p2pmg_kernels.hip)
+    auto in = [](double x, double lo, double hi) { return x >= lo && x <= hi; };
+    const double se = std::sqrt(efficiency);
+    bool ok = in(min_soc, 0x1p-100, 0x1p10) && in(max_soc, 0x1p-100, 0x1p10) && in(se, 0x1p-10, 0x1p10);
+    for (size_t a = 0; a < A && ok; ++a) {
+      ok = capacity[a] == 0.0 || in(capacity[a], 0x1p-20, 0x1p60);
+      ok = ok && in(soc0 ? soc0[a] : 0.5, 0.0, 0x1p10);
+    }
+    c->bat_domain = ok;
+  }
   c->battery = true;
   c->bat_min = min_soc;
   c->bat_max = max_soc;

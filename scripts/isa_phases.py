@@ -62,9 +62,9 @@ def main(path, sym, phase_map=None):
         if m:
             loc = (files.get(int(m.group(1)), "?"), int(m.group(2)))
             continue
-        if re.match(r"^\.LBB\S*:", s) or re.match(r"^\.Ltmp\S*:", s) and False:
+        if re.match(r"^\.LBB\S*:", s) or re.match(r"^; %bb\.\d+:", s):
             blocks.append(cur)
-            cur = {"label": s.rstrip(":").split()[0], "n": collections.Counter(), "phases": collections.Counter(),
+            cur = {"label": s.split(":")[0] if not s.startswith(";") else s.split()[1].rstrip(":"), "n": collections.Counter(), "phases": collections.Counter(),
                    "branches": []}
             continue
         if not s or s.startswith((".", ";")) or s.endswith(":"):
