@@ -627,10 +627,18 @@ def main():
         issue = issue_roofline(args.workload, kernel_ms)
         if issue:
             out["roofline"]["issue"] = issue
+        # What binds the kernel: achieved/peak/frac above stay the HBM roofline
+        # (algorithmic bytes); "bound" names the limit the measurements point to and
+        # "binding_frac" is the fraction against that limit.
         if not (shared or battery or hetero) and q_dtype == "f64" and N == 2 and R == 1:
             gather = gather_roofline(S * N, T, kernel_ms)
             if gather:
                 out["roofline"]["gather_floor"] = gather
+                out["roofline"]["bound"] = "latency"  # one wave per CU: the dependent row-gather chain
+                out["roofline"]["binding_frac"] = gather["frac"]
+        elif shared and issue and issue["frac"] > 0.5:
+            out["roofline"]["bound"] = "valu-issue"  # every SIMD busy: VALU instructions per agent-step
+            out["roofline"]["binding_frac"] = issue["frac"]
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args.cpu_seconds, S=(64 if hetero else 256) if N <= 4 else 64,
                               N=N, R=R, T=T, q_dtype=q_dtype, shared=shared, battery=battery,

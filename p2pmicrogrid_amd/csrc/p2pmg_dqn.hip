@@ -70,6 +70,39 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ReplayBuffer.sample_batch rl.py:226-241 for every agent of the step, ahead of the train kernel:
+// one wave per agent draws 32 distinct deque indices (replayed, or Philox + Floyd as in
+// oracle/philox.py::sample_draws) and writes their ring slots to d.smp (as int32 [A][32]); the
+// train kernel gathers each agent's 32 transitions from the ring one agent ahead (double-buffered),
+// so neither kernel waits on the random ring reads behind the serial 32-step selection loop.
+// One wave draws agent a's 32 slots; n_added = the agent's transitions including this step's.
+__device__ __forceinline__ void sample_slots(const DqnParams& d, int a, int l, int n_added) {
+  const EpisodeParams& p = d.e;
+  const size_t A = (size_t)p.A;
+  const int count = n_added < d.cap ? n_added : d.cap;
+  const int first = n_added - count;
+  int idx = 0;
+  if (d.samples) {
+    idx = l < kB ? (int)d.samples[((size_t)d.t * A + a) * kB + l] : 0;
+  } else {
+    uint32_t c0 = (uint32_t)d.t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
+             c3 = kTagSample + (uint32_t)(l & 31);
+    philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
+    const int mj = count - kB + (l & 31);
+    const int rj = (int)__umulhi(c0, (uint32_t)(mj + 1));
+    idx = rj;
+    for (int j = 0; j < kB; ++j) {
+      const int r = __builtin_amdgcn_readlane(rj, j);  // lane j's draw (j is uniform: an SGPR read, no LDS trip)
+      const bool taken = __ballot(l < j && idx == r) != 0;
+      if (l == j) idx = taken ? count - kB + j : r;
+    }
+  }
+  if (l < kB) reinterpret_cast<int*>(d.smp)[(size_t)a * kB + l] = (first + idx) % d.cap;
+}
+__global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
+  sample_slots(d, blockIdx.x, threadIdx.x, d.added[blockIdx.x]);
+}
+
 // ----------------------------------------------------------------- act: one env step
 template <int N>
 __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
@@ -221,6 +254,9 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
       slot[lane] = v;
     }
     if (lane == 0) d.added[a] = n_added + 1;
+    // Trainer.train -> ReplayBuffer.sample_batch (rl.py:299-305, 226-241) right after the append
+    // (agent.py:338-342): the same wave draws the agent's 32 slots, no separate launch
+    if (p.mode == 0 && d.fused_sample) sample_slots(d, a, lane, n_added + 1);
   }
   if (lane == 0) {
     const size_t k = (size_t)t * A + a;
@@ -259,36 +295,6 @@ __device__ __forceinline__ void adam_update(const DqnParams& d, float* th, float
   tg[idx] = d.tau_c * tg[idx] + d.tau * w;
 }
 
-// ReplayBuffer.sample_batch rl.py:226-241 for every agent of the step, ahead of the train kernel:
-// one wave per agent draws 32 distinct deque indices (replayed, or Philox + Floyd as in
-// oracle/philox.py::sample_draws) and writes their ring slots to d.smp (as int32 [A][32]); the
-// train kernel gathers each agent's 32 transitions from the ring one agent ahead (double-buffered),
-// so neither kernel waits on the random ring reads behind the serial 32-step selection loop.
-__global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
-  const EpisodeParams& p = d.e;
-  const int a = blockIdx.x, l = threadIdx.x;
-  const size_t A = (size_t)p.A;
-  const int n_added = d.added[a];
-  const int count = n_added < d.cap ? n_added : d.cap;
-  const int first = n_added - count;
-  int idx = 0;
-  if (d.samples) {
-    idx = l < kB ? (int)d.samples[((size_t)d.t * A + a) * kB + l] : 0;
-  } else {
-    uint32_t c0 = (uint32_t)d.t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
-             c3 = kTagSample + (uint32_t)(l & 31);
-    philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-    const int mj = count - kB + (l & 31);
-    const int rj = (int)__umulhi(c0, (uint32_t)(mj + 1));
-    idx = rj;
-    for (int j = 0; j < kB; ++j) {
-      const int r = __builtin_amdgcn_readlane(rj, j);  // lane j's draw (j is uniform: an SGPR read, no LDS trip)
-      const bool taken = __ballot(l < j && idx == r) != 0;
-      if (l == j) idx = taken ? count - kB + j : r;
-    }
-  }
-  if (l < kB) reinterpret_cast<int*>(d.smp)[(size_t)a * kB + l] = (first + idx) % d.cap;
-}
 
 // one thread's share of agent a's sampled batch (thread t: sample t / 8, floats t % 8 and, for
 // t % 8 < 2, t % 8 + 8), gathered from the replay ring through the sample kernel's slot indices

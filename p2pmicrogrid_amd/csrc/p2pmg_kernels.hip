@@ -1086,7 +1086,8 @@ struct FastRec {         // [T][A], 32 B
   uint32_t bins;         // (it * nT*nb + ib) | iT << 16
   uint32_t ips;          // byte r: p2p bin of round r
 };
-template <int N, typename QT, int R1, bool TRAIN, bool BAT, bool NARROW>
+// BAT: 0 none, 1 battery with per-lane range tests, 2 battery in the launcher-verified domain
+template <int N, typename QT, int R1, bool TRAIN, int BAT, bool NARROW>
 __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams p, const uint2* __restrict__ pre,
                                                              FastRec* __restrict__ recs, int spw, int n_cons,
                                                              const PrepOut nxt) {
@@ -1103,7 +1104,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   // N = 2: round 1's Q row is one of three (by the partner's round-0 action) whose bins the
   // pre-pass wrote; all three are issued a step ahead, so round 1 waits for no gather
   // (not with a battery: the partner's round-0 power then depends on its state of charge)
-  constexpr bool CAND = N == 2 && R1 >= 2 && !BAT;
+  constexpr bool CAND = N == 2 && R1 >= 2 && BAT == 0;
   const int lane = (int)threadIdx.x;
   const int sl = lane / G;
   const int i = lane % G;
@@ -1142,7 +1143,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   double bcap = 0.0, soc = 0.0;
   BatK bk{};
   Recip64 rcap{};
-  if constexpr (BAT) {
+  if constexpr (BAT != 0) {
     bcap = active ? p.bat_cap[a] : 0.0;
     soc = active ? p.soc[a] : 0.0;
     bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64_u(p.bat_sqrt_eff), recip64_u(900.0)};
@@ -1341,8 +1342,8 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     }
     float out0 = balw + hp;
     double soc_r = soc;  // tentative SoC of the current round
-    if constexpr (BAT) {
-      if (bcap > 0.0) out0 = (float)battery_rule_r((double)out0, soc_r, bcap, rcap, bk);
+    if constexpr (BAT != 0) {
+      if (bcap > 0.0) out0 = (float)battery_rule_r<BAT == 1>((double)out0, soc_r, bcap, rcap, bk);
     }
     const float ev0 = div_n_r<N>(out0 * 1.0f, rn);
 #pragma unroll
@@ -1408,9 +1409,9 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         settle_next();
       }
       float out = balw + hp;
-      if constexpr (BAT) {
+      if constexpr (BAT != 0) {
         soc_r = soc;
-        if (bcap > 0.0) out = (float)battery_rule_r((double)out, soc_r, bcap, rcap, bk);
+        if (bcap > 0.0) out = (float)battery_rule_r<BAT == 1>((double)out, soc_r, bcap, rcap, bk);
       }
 #if P2PMG_ABLATE == 11  // timing-only: no final-round divide-power and no market (cost from out alone)
       if (r == R1 - 1) {
@@ -1552,7 +1553,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       t0_draw(p.seed_lo, p.seed_hi, p.episode + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, tin, tm);
     p.t_in[a] = tin;
     p.t_m[a] = tm;
-    if constexpr (BAT) p.soc[a] = soc;
+    if constexpr (BAT != 0) p.soc[a] = soc;
     if (i == 0) p.ep_reward[s] = ep_sum;
   }
 }
@@ -1589,7 +1590,7 @@ __global__ void fast_rec_unpack_kernel(int T, int R1, int A, uint32_t tb, const 
 
 // hipExtLaunchKernel stamps the start / stop events from the dispatch itself: no marker packets
 // between back-to-back episodes
-template <int N, typename QT, int R1, bool BAT, bool NARROW>
+template <int N, typename QT, int R1, int BAT, bool NARROW>
 void launch_fast_nw(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
                     const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
   if (p.mode == 0)
@@ -1599,7 +1600,7 @@ void launch_fast_nw(const EpisodeParams& p, const uint2* pre, FastRec* recs, int
     hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, false, BAT, NARROW>), dim3(blocks + prod), dim3(kWave), 0, st,
                           ev0, ev1, 0, p, pre, recs, spw, blocks, nxt);
 }
-template <int N, typename QT, int R1, bool BAT>
+template <int N, typename QT, int R1, int BAT>
 void launch_fast_b(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
                    const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
   if (p.rec_narrow) return launch_fast_nw<N, QT, R1, BAT, true>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
@@ -1609,9 +1610,10 @@ template <int N, typename QT, int R1>
 void launch_fast_r(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
                    const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
   if constexpr (R1 <= kFastBatMaxR1) {
-    if (p.battery) return launch_fast_b<N, QT, R1, true>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
+    if (p.battery && p.bat_safe) return launch_fast_b<N, QT, R1, 2>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
+    if (p.battery) return launch_fast_b<N, QT, R1, 1>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
   }
-  launch_fast_b<N, QT, R1, false>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
+  launch_fast_b<N, QT, R1, 0>(p, pre, recs, blocks, spw, prod, nxt, ev0, ev1, st);
 }
 
 template <int N, typename QT>
@@ -1978,11 +1980,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     wave_lds_fence();
     ep_sum = ep_sum + div_n<N>(msum);
     if constexpr (TRAIN) {
-#if P2PMG_SQ_ABL == 2
-      if (t + 1 == T)  // timing-only ablation: one flush at the end
-#else
       if (t % kSqFlushSteps == kSqFlushSteps - 1 || t + 1 == T)
-#endif
         lds_hash_flush(hkey, hval, dbase, kSq16Waves * kWave);
     }
 

@@ -773,7 +773,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   c->last_kernel = std::string(fast ? "episode_fast_kernel<" : sq16 ? "episode_sq16_kernel<" : "episode_kernel<") +
                    std::to_string(c->N) + "," + (g.q_dtype == 0 ? "f64" : "f32") + ",R1=" + std::to_string(c->R + 1) +
                    (ext ? (train ? ",train" : ",greedy") : "") + (g.shared_q ? ",shared" : "") +
-                   (c->battery ? ",battery>" : ">");
+                   (c->battery ? (ext && !p.bat_safe ? ",battery,range-checked>" : ",battery>") : ">");
   if (!ext && stamp) HIP_TRY(c, hipEventRecord(r1, c->stream));
   if (fast) c->pslot ^= 1;
   if (reset && !ext) {  // general kernel: the reset as its own launch
@@ -1510,7 +1510,7 @@ static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
   for (auto& st : c->d_steps) ++st;
   d.lr_t = adam_lr(c->dcfg, c->d_steps[0]);
   d.lr_net = same ? nullptr : c->d_lr + (size_t)d.t * c->d_steps.size();
-  HIP_TRY(c, p2pmg::launch_dqn_sample(d, c->stream));
+  if (!d.fused_sample) HIP_TRY(c, p2pmg::launch_dqn_sample(d, c->stream));
   if (c->n_nets == 1) {
     HIP_TRY(c, p2pmg::launch_dqn_train(d, c->d_blocks, true, c->stream));
     const bool ranks = c->comm && c->nranks > 1;
@@ -1554,6 +1554,7 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     c->ring.assign(2 * p2pmg_ctx::kRing, nullptr);
     for (auto& ev : c->ring) HIP_TRY(c, hipEventCreate(&ev));
   }
+  d.fused_sample = (mode == P2PMG_MODE_TRAIN) ? 1 : 0;  // the act launch of each env step draws the samples
   const bool same = mode != P2PMG_MODE_TRAIN || dqn_steps_same(c);
   if (!same) {
     rc = dqn_upload_lr_table(c);

@@ -162,3 +162,27 @@ def test_sq16_kernel_matches_general_kernel(q_dtype, battery, R):
     for k in ("reward", "cost"):
         assert np.array_equal(a.get_record(k), b.get_record(k)), ("narrow", k)
     assert np.array_equal(a.get_q_delta(), b.get_q_delta())
+
+
+@pytest.mark.parametrize("N,shared", [(4, False), (16, True)])
+def test_battery_outside_verified_domain_takes_checked_rule(N, shared):
+    """The fast / sq16 kernels drop the battery rule's per-lane range tests only inside the operand
+    domain the runtime verifies (p2pmg_set_battery / set_profiles); one tiny battery (2^-30 J, below
+    the verified capacities) selects the range-checked variant, which still equals the oracle."""
+    S, R, T = 24, 1, 32
+    q_dtype = "f32" if shared else "f64"
+    eng, ob = _setup(S, N, R, T, q_dtype, shared, True, False, seed=5)
+    for e in range(3):
+        if e == 1:  # the same community from here on with one tiny battery
+            cap = np.full((S, N), 10 * 3.6e6)
+            cap[0, 0] = 2.0 ** -30
+            eng.set_battery(cap, 0.1, 0.9, 0.9, soc0=eng.get_soc())
+            ob.battery_capacity = cap.copy()
+        eng.run_episode("train", "philox", episode=e, epsilon=0.6, record=REC)
+        assert ("range-checked" in eng.last_kernel()) == (e >= 1), eng.last_kernel()
+        out = ob.run_episode("train", rng="philox", episode=e, eps=0.6)
+        _cmp(out, eng.get_records(REC), ("checked", N, e))
+        assert np.array_equal(eng.get_soc(), ob.soc), e
+        if shared:
+            eng.apply_q_delta()
+            ob.apply_q_delta()
