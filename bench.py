@@ -50,6 +50,29 @@ def algorithmic_bytes_per_agent_step(R: int, q_bytes: int, outputs: int = 2) -> 
     return 8 + q_bytes * (3 * (R + 1) + 3 + 2) + 4 * outputs
 
 
+def sector_model_per_agent_step(N: int, R: int, eps: float, battery: bool, q_bytes: int = 8):
+    """The HBM bytes the fast per-agent-table kernel moves per agent-step at the memory system's
+    32-B sector granularity (what the FETCH_SIZE / WRITE_SIZE passes count), next to the
+    algorithmic bytes of SURVEY §8(d).  Components (p2pmg_kernels.hip::episode_fast_kernel):
+    reads -- the profile pair (8 B, coalesced), the step pre-pass word (8 B), the exploration code
+    word (4 B), for N = 2 without a battery the round-1 bins word (4 B); Q rows as whole sectors:
+    round 0's row only when round 0 is greedy (1 - eps), the round-1 row(s) (3 candidates for N = 2
+    without a battery, else the one dependent row), the next-state row; the producer blocks' re-read
+    of the profiles for the next episode's pre-pass (8 B).  Writes -- the TD store (8 B landing in a
+    32-B sector), the {reward, cost} record row (8 B), the next episode's pre-pass words (8 + 4 B,
+    + 4 B of bins for the N = 2 path).  The Q-row sectors and the TD sector are the 2x over the
+    algorithmic bytes that the PMC traffic shows (VERDICT r02 'wasted traffic')."""
+    sector = 32 if q_bytes == 8 else 16
+    cand = N == 2 and R >= 1 and not battery
+    rows = (1.0 - eps) + (3 if cand else R) + 1
+    reads = {"profile": 8, "prepass_word": 8, "code_word": 4, "round1_bins": 4 if cand else 0,
+             "q_rows_sectors": rows * sector, "producer_profile_reread": 8}
+    writes = {"td_store_sector": 32, "record_row": 8, "next_prepass_words": 12 + (4 if cand else 0)}
+    return {"read": reads, "write": writes, "read_total": sum(reads.values()), "write_total": sum(writes.values()),
+            "total": sum(reads.values()) + sum(writes.values()), "epsilon": eps,
+            "note": "per agent-step, at 32-B sectors; q_rows = (1 - eps) round-0 row + round-1 row(s) + next-state row"}
+
+
 def algorithmic_bytes_per_agent_step_shared(agents: int, q_bytes: int, battery: bool, outputs: int = 2) -> float:
     """SURVEY.md §8(d), shared table: 8 (load_w, pv_w) + 4 * outputs + the table read once and its
     int64 delta buffer read+written once per step, amortised over the agents of the step
@@ -624,6 +647,11 @@ def main():
             assert out["table_replicas_identical"], f"shared-table replicas differ across ranks: {hashes}"
         if traffic:
             out["roofline"]["traffic_source"] = traffic.get("source")
+        if not shared and q_dtype == "f64" and N <= 8:  # the fast kernel's sector-granular traffic model
+            eps_mid = epsilon_at(args.warmup + args.steps // 2)
+            sm = sector_model_per_agent_step(N, R, eps_mid, battery or hetero)
+            sm["bytes_per_launch"] = sm["total"] * steps_per_episode
+            out["roofline"]["sector_model"] = sm
         issue = issue_roofline(args.workload, kernel_ms)
         if issue:
             out["roofline"]["issue"] = issue

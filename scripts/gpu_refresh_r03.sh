@@ -1,0 +1,57 @@
+#!/bin/bash
+# Round-3 profile refresh at HEAD: the bench line of every workload (with its CPU baseline), the
+# launcher's --gpus 2 rehearsal, rocprofv3 kernel stats, FETCH_SIZE / WRITE_SIZE in separate --pmc
+# passes for the configs[1], [2], [3] episode kernels, SQ counter passes (configs[1], [2]) and the
+# instruction-rate microbenchmark.  Stops at the first failure.  scripts/summarize_r03.py -> profiles/.
+# usage: gpu_refresh_r03.sh [A|B]  (A: bench lines, microbenchmark, kernel stats; B: PMC + SQ passes)
+R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
+O="$R/gpurun_out/r03"; mkdir -p "$O"
+PART="${1:-A}"
+run() {  # name timeout args...
+  local n=$1 to=$2; shift 2
+  timeout -k 10 "$to" python -u bench.py "$@" > "$O/$n.json" 2> "$O/$n.err" || { tail -20 "$O/$n.err"; exit 1; }
+  tail -c 300 "$O/$n.json"; echo
+}
+if [ "$PART" = A ]; then
+run c2 300 --steps 200 --warmup 10
+run c2n2 300 --gpus 2 --steps 200 --warmup 10 --no-cpu-baseline
+run c3 400 --workload config3 --steps 10 --warmup 2
+run c4 500 --workload config4 --steps 3 --warmup 1
+run c5 400 --workload config5 --steps 10 --warmup 2
+timeout -k 10 120 ./build/ubench_rate > "$O/ubench_rate.jsonl" 2>&1 || { tail -5 "$O/ubench_rate.jsonl"; exit 1; }
+fi
+cd /tmp && export TMPDIR=/tmp
+prof() {  # name timeout args...
+  local n=$1 to=$2; shift 2
+  timeout -k 10 "$to" rocprofv3 --kernel-trace --stats -d "$O/prof_$n" -o "$n" --output-format csv -- python3 "$R/bench.py" "$@" --no-cpu-baseline > "$O/prof_$n.log" 2>&1 || { tail -20 "$O/prof_$n.log"; exit 1; }
+}
+pmc() {  # name counters timeout args...
+  local n=$1 c=$2 to=$3; shift 3
+  timeout -s KILL "$to" rocprofv3 --pmc $c --kernel-trace -d "$O/pmc_${n}_${c%% *}" -o "${c%% *}" --output-format csv -- python3 "$R/bench.py" "$@" --no-cpu-baseline > "$O/pmc_${n}_${c%% *}.log" 2>&1 || { tail -20 "$O/pmc_${n}_${c%% *}.log"; exit 1; }
+}
+if [ "$PART" = A ]; then
+prof c2 300 --steps 30 --warmup 3
+prof c3 300 --workload config3 --steps 4 --warmup 1
+prof c4 500 --workload config4 --steps 2 --warmup 1
+prof c5 300 --workload config5 --steps 3 --warmup 1
+echo done A
+exit 0
+fi
+pmc c2 FETCH_SIZE 200 --steps 6 --warmup 1
+pmc c2 WRITE_SIZE 200 --steps 6 --warmup 1
+pmc c3 FETCH_SIZE 300 --workload config3 --steps 2 --warmup 1
+pmc c3 WRITE_SIZE 300 --workload config3 --steps 2 --warmup 1
+pmc c4 FETCH_SIZE 400 --workload config4 --steps 1 --warmup 1
+pmc c4 WRITE_SIZE 400 --workload config4 --steps 1 --warmup 1
+# SQ issue counters (two passes of <= 8 SQ counters), producer blocks off (P2PMG_NO_SPEC=1)
+export P2PMG_NO_SPEC=1
+PA="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
+PB="SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VALU"
+for W in config2 config3; do
+  ST=8; [ $W = config3 ] && ST=2
+  for P in A B; do
+    C=$PA; [ $P = B ] && C=$PB
+    timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace -d "$O/sq/${W}_$P" -o p --output-format csv -- python3 "$R/bench.py" --workload $W --steps $ST --warmup 1 --no-cpu-baseline > "$O/sq_${W}_$P.log" 2>&1 || { tail -20 "$O/sq_${W}_$P.log"; exit 1; }
+  done
+done
+echo done
