@@ -63,6 +63,24 @@ __device__ __forceinline__ float sum_groups(float v) {  // over the 4 row groups
   return plus_swap32(plus_swap16(v));
 }
 __device__ __forceinline__ float wave_sum(float v) { return sum_groups(sum16(v)); }
+// sum over the 4 row groups of four values at once: the first swaps pair row groups (g4, g4 ^ 1)
+// of (a, b) and of (c, d), the second (g4, g4 ^ 2) of the two pair sums, so each row group ends
+// holding ONE tile's total ((g0 + g1) + (g2 + g3), sum_groups' tree); reduce4_tag() says which
+// (the same swaps applied to the tile numbers)
+__device__ __forceinline__ float reduce4_groups(float a, float b, float c, float d) {
+  const auto r1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  const auto r2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(c), __float_as_uint(d), false, false);
+  const float ab = __uint_as_float(r1[0]) + __uint_as_float(r1[1]);
+  const float cd = __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+  const auto r3 = __builtin_amdgcn_permlane32_swap(__float_as_uint(ab), __float_as_uint(cd), false, false);
+  return __uint_as_float(r3[0]) + __uint_as_float(r3[1]);
+}
+__device__ __forceinline__ int reduce4_tag() {
+  const auto r1 = __builtin_amdgcn_permlane16_swap(0u, 1u, false, false);
+  const auto r2 = __builtin_amdgcn_permlane16_swap(2u, 3u, false, false);
+  const auto r3 = __builtin_amdgcn_permlane32_swap(r1[0], r2[0], false, false);
+  return (int)r3[0];
+}
 
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -281,6 +299,285 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
   }
 }
 
+// ----------------------------------------------------------------- act, one shared network
+// dqn_act_shared_kernel<N>: the same env step as dqn_act_kernel for ONE network shared by every
+// agent (configs[4]), with the greedy forwards of 16 agents on MFMA tiles.  A 256-thread workgroup
+// owns kActAgents / N scenarios (16 agents).  Per round, thread j < 16 does agent j's scalar work
+// (observation, exploration draw, divide-power row); the 48 greedy rows (3 actions x 16 agents) go
+// through layer 1 on VALU (thread = hidden unit x 4 agents), layer 2 as Z2^T = W2^T H1^T on
+// v_mfma_f32_16x16x4_f32 (wave w owns hidden units 16w..16w+15; its 16 W2 operands stay in
+// registers for the launch; the shared W2 is read once per workgroup instead of once per agent and
+// round), layer 3 in-lane.  Bitwise the same Q values as dqn_act_kernel: the f32 MFMA accumulates
+// its K products as an fmaf chain in k order (the VALU loop's order), and layer 3's sum over the 64
+// units is the same pairwise tree (4 units in-lane, the 16-lane row groups over lane ^ 16 and
+// lane ^ 32, then the 4 waves pairwise) as wave_sum over lane = unit.
+constexpr int kActAgents = 16;
+constexpr int kActRows = 3 * kActAgents;  // row = action * 16 + agent slot
+
+// ReplayBuffer.sample_batch (rl.py:226-241) for two agents in one wave: lanes 0..31 draw agent a0's
+// 32 slots, lanes 32..63 agent a1's (sample_slots's Floyd loop with half-wave ballots)
+__device__ __forceinline__ void sample_slots2(const DqnParams& d, int a0, int a1, bool v0, bool v1, int l, int n0,
+                                              int n1) {
+  const EpisodeParams& p = d.e;
+  const size_t A = (size_t)p.A;
+  const bool hi = l >= 32;
+  const int jl = l & 31;
+  const int a = hi ? a1 : a0;
+  const int n_added = hi ? n1 : n0;
+  const int count = n_added < d.cap ? n_added : d.cap;
+  const int first = n_added - count;
+  int idx = 0;
+  if (d.samples) {
+    idx = (hi ? v1 : v0) ? (int)d.samples[((size_t)d.t * A + a) * kB + jl] : 0;
+  } else {
+    uint32_t c0 = (uint32_t)d.t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a, c3 = kTagSample + (uint32_t)jl;
+    philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
+    const int mj = count - kB + jl;
+    const int rj = (int)__umulhi(c0, (uint32_t)(mj + 1));
+    idx = rj;
+    for (int j = 0; j < kB; ++j) {
+      const int rlo = __builtin_amdgcn_readlane(rj, j), rhi = __builtin_amdgcn_readlane(rj, j + 32);
+      const int r = hi ? rhi : rlo;
+      const uint64_t m = __ballot(jl < j && idx == r);
+      const bool taken = hi ? (m >> 32) != 0 : (uint32_t)m != 0;
+      if (jl == j) idx = taken ? count - kB + j : r;
+    }
+  }
+  if (hi ? v1 : v0) reinterpret_cast<int*>(d.smp)[(size_t)a * kB + jl] = (first + idx) % d.cap;
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) {
+  constexpr int SPW = kActAgents / N;  // scenarios per workgroup
+  constexpr int AG = SPW * N;          // agents per workgroup (<= 16)
+  const EpisodeParams& p = d.e;
+  __shared__ float shP[2][AG * N];
+  __shared__ float4 shX[kActAgents];   // time, normalised T_in, balance, p2p of agent slot j
+  __shared__ float H1[kActRows][kLdsRow];
+  __shared__ float qpart[4][kActRows + 16];  // + the 4th (unused) tile of reduce4_groups
+  __shared__ float shR[AG];
+  __shared__ int shN[kActAgents];
+  const int tid = threadIdx.x;
+  const int w = tid / kWave, l = tid % kWave;
+  const int c16 = l & 15, g4 = l >> 4;
+  const int t = d.t, T = p.T, tn = (t + 1 == T) ? 0 : t + 1;
+  const int R1 = p.R + 1, W = (R1 + 3) >> 2;
+  const size_t A = (size_t)p.A;
+  const bool greedy_mode = p.mode == 1;
+  const int s0 = blockIdx.x * SPW;
+  const float* th = d.theta;
+
+  // agent thread j < AG: agent a = s0 * N + j of scenario s0 + j / N (agent i = j % N)
+  const int j = tid;
+  const int sl = j / N, i = j % N;
+  const int s = s0 + sl;
+  const bool agent_thr = j < AG && s < p.S;
+  const int a = agent_thr ? s * N + i : 0;
+  const int s_env = p.n_env == 1 ? 0 : (agent_thr ? s : 0);
+  const float* e0 = p.env + ((size_t)t * p.n_env + s_env) * kEnvStride;
+  const float* e1 = p.env + ((size_t)tn * p.n_env + s_env) * kEnvStride;
+  float time_t = 0.0f, t_out = 0.0f, time_n = 0.0f, mi = 1.0f, tin = 0.0f, tm = 0.0f, bal = 0.0f, baln = 0.0f,
+        tnorm = 0.0f;
+  float4 lv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (agent_thr) {
+    time_t = e0[0];
+    t_out = e0[1];
+    time_n = e1[0];
+    const float2 f0 = p.prof[(size_t)t * A + a], f1 = p.prof[(size_t)tn * A + a];
+    mi = p.max_in[a];
+    tin = p.t_in[a];
+    tm = p.t_m[a];
+    bal = (f0.x - f0.y) / mi;  // RLAgent._get_balance agent.py:172-176
+    baln = (f1.x - f1.y) / mi;
+    tnorm = (tin - p.setpoint) / p.margin;  // HPHeating.normalized_temperature heating.py:118-120
+    lv = p.hp_lv[a];
+  }
+  // layer 1 (thread = hidden unit u of agent slots 4 * (tid / 64) .. + 3): W1 column and b1
+  const int u = l;
+  const float w10 = th[kOffW1 + 0 * kH + u], w11 = th[kOffW1 + 1 * kH + u], w12 = th[kOffW1 + 2 * kH + u],
+              w13 = th[kOffW1 + 3 * kH + u], w14 = th[kOffW1 + 4 * kH + u], b1 = th[kOffB1 + u];
+  // layer 2 / 3 (wave w, lane: A operand W2[4 kk + g4][16 w + c16]; accumulator units 16 w + 4 g4 + r)
+  float w2[16];
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) w2[kk] = th[kOffW2 + (4 * kk + g4) * kH + 16 * w + c16];
+  float b2[4], w3[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    b2[r] = th[kOffB2 + 16 * w + 4 * g4 + r];
+    w3[r] = th[kOffW3 + 16 * w + 4 * g4 + r];
+  }
+  const float b3 = th[kOffB3];
+  const int tag4 = reduce4_tag();
+
+  if (tid < AG * N) shP[0][tid] = 0.0f;
+  __syncthreads();
+  int cur = 0, act = 0, code = 255;
+  float hp = 0.0f, p2pf = 0.0f;
+  for (int r = 0; r < R1; ++r) {
+    const float* P = shP[cur] + sl * N * N;  // this agent's scenario
+    bool greedy = false;
+    if (agent_thr) {
+      // powers = -P[:, i], diagonal zeroed (community.py:76,81); p2p = mean / max_in (agent.py:203)
+      float acc = 0.0f;
+#pragma unroll
+      for (int jj = 0; jj < N; ++jj) acc = acc + (-((jj == i) ? 0.0f : P[jj * N + i]));
+      p2pf = div_n<N>(acc) / mi;
+      code = 255;  // ActorModel.select_action rl.py:174-183: explore draw, else greedy
+      if (!greedy_mode) {
+        if (p.rng == 0) {
+          code = (int)((p.codes[((size_t)t * W + (r >> 2)) * A + a] >> (8 * (r & 3))) & 0xFFu);
+        } else {
+          uint32_t c0 = (uint32_t)(t * ((R1 + 1) >> 1) + (r >> 1)), c1 = (uint32_t)p.episode,
+                   c2 = p.agent_offset + (uint32_t)a, c3 = kTagDecision;
+          philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
+          const uint32_t wu = (r & 1) ? c2 : c0, wa = (r & 1) ? c3 : c1;
+          code = (double)wu * (1.0 / 4294967296.0) < p.eps ? (int)__umulhi(wa, 3u) : 255;
+        }
+      }
+      greedy = code == 255;
+      shX[j] = make_float4(time_t, tnorm, bal, p2pf);
+    }
+    if (__syncthreads_or(greedy)) {
+      // layer 1: the three action rows of agent slots 4 (tid / 64) .. + 3 at unit u
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ag = 4 * w + q;
+        const float4 x = shX[ag];
+        float z = x.w * w13;
+        z = fmaf(x.z, w12, z);
+        z = fmaf(x.y, w11, z);
+        z = fmaf(x.x, w10, z);
+        H1[ag][u] = relu(z + b1);
+        H1[kActAgents + ag][u] = relu(fmaf(0.5f, w14, z) + b1);
+        H1[2 * kActAgents + ag][u] = relu((z + w14) + b1);
+      }
+      __syncthreads();
+      f32x4 acc[3];
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt) acc[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt) acc[rt] = mfma4(w2[kk], H1[16 * rt + c16][4 * kk + g4], acc[rt]);
+      float sq[3];
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = relu(acc[rt][q] + b2[q]) * w3[q];
+        sq[rt] = (v[0] + v[1]) + (v[2] + v[3]);  // wave_sum's tree: 4 units in-lane, ...
+      }
+      qpart[w][16 * tag4 + c16] = reduce4_groups(sq[0], sq[1], sq[2], 0.0f);  // ... the 4 row groups
+      __syncthreads();
+    }
+    if (agent_thr) {
+      if (greedy) {
+        // ActorModel.greedy_action rl.py:188-196: Q(obs, a) for a in (0, .5, 1), argmax (first max)
+        float qv[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int row = 16 * k + j;
+          qv[k] = ((qpart[0][row] + qpart[1][row]) + (qpart[2][row] + qpart[3][row])) + b3;
+        }
+        act = 0;
+        float best = qv[0];
+        if (qv[1] > best) { best = qv[1]; act = 1; }
+        if (qv[2] > best) act = 2;
+      } else {
+        act = code;
+      }
+      hp = act == 0 ? lv.x : (act == 1 ? lv.y : lv.z);  // heating.set_power(action) -> hp.power * max_power
+      // RLAgent._divide_power agent.py:186-195 on out = balance * max_in + hp (agent.py:210)
+      const float out = (bal * mi) + hp;
+      const float so = sgn(out);
+      float f[N];
+      float tot = 0.0f;
+#pragma unroll
+      for (int jj = 0; jj < N; ++jj) {
+        const float pw = -((jj == i || r == 0) ? 0.0f : P[jj * N + i]);
+        f[jj] = (so != sgn(pw)) ? pw : 0.0f;
+        tot = tot + f[jj];
+      }
+      tot = fabsf(tot);
+      float* Pn = shP[cur ^ 1] + sl * N * N + i * N;
+#pragma unroll
+      for (int jj = 0; jj < N; ++jj) {
+        float v;
+        if (tot == 0.0f) v = div_n<N>(out * 1.0f);
+        else v = (jj == i) ? (tot == tot ? out * 0.0f : tot) : (out * fabsf(f[jj])) / tot;
+        Pn[jj] = v;
+      }
+      if (p.record & 32) p.rec_action[((size_t)t * R1 + r) * A + a] = (uint8_t)act;
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (agent_thr) {
+    // CommunityMicrogrid._assign_powers community.py:45-54 (final P, diagonal kept)
+    const float* P = shP[cur] + sl * N * N;
+    float g = 0.0f, pp = 0.0f;
+#pragma unroll
+    for (int jj = 0; jj < N; ++jj) {
+      const float pij = P[i * N + jj], pji = P[jj * N + i];
+      const float ex = __builtin_amdgcn_fmed3f(pij, -pji, 0.0f);  // pair_exchange (p2pmg_kernels.hip)
+      g = g + (pij - ex);
+      pp = pp + ex;
+    }
+    // _compute_costs community.py:56-65; RLAgent.get_reward agent.py:225-232 (pre-update T_in)
+    const float buy = e0[2], inj = e0[3], p2pp = e0[4];
+    float cost = (g >= 0.0f) ? g * buy : g * inj;
+    cost = cost + pp * p2pp;
+    cost = (cost * p.slot) / p.mph;
+    cost = cost * p.kilo;
+    float pen = fmaxf(fmaxf(0.0f, p.lower - tin), fmaxf(0.0f, tin - p.upper));
+    pen = pen > 0.0f ? pen + 1.0f : 0.0f;
+    const float rw = -(cost + p.penw * pen);
+    if (p.mode != 1) {
+      // DQNAgent.save_memory agent.py:332-336 -> ReplayBuffer.add rl.py:208-212
+      const int32_t n_added = d.added[a];
+      float2* slot = reinterpret_cast<float2*>(d.buf + ((size_t)a * d.cap + (size_t)(n_added % d.cap)) * kTrans);
+      const float av = act == 0 ? 0.0f : (act == 1 ? 0.5f : 1.0f);
+      slot[0] = make_float2(time_t, tnorm);
+      slot[1] = make_float2(bal, p2pf);
+      slot[2] = make_float2(av, rw);
+      slot[3] = make_float2(time_n, tnorm);  // next state: same (pre-update) temperature (community.py:161)
+      slot[4] = make_float2(baln, 0.0f / mi);  // next state p2p = mean(zeros) / max_in
+      d.added[a] = n_added + 1;
+      shN[j] = n_added + 1;
+    }
+    const size_t k = (size_t)t * A + a;
+    if (p.record & 1) p.rec_reward[k] = rw;
+    if (p.record & 2) p.rec_cost[k] = cost;
+    if (p.record & 4) p.rec_grid[k] = g;
+    if (p.record & 8) p.rec_p2p[k] = pp;
+    if (p.record & 16) p.rec_tin[k] = tin;
+    rc_update(p, t_out, hp, tin, tm);  // HPHeating.step heating.py:138-143
+    p.t_in[a] = tin;
+    p.t_m[a] = tm;
+    shR[j] = rw;
+  }
+  __syncthreads();
+  if (tid < SPW && s0 + tid < p.S) {  // avg_reward = sum_t mean_i r (community.py:179), canonical order
+    const int sc = s0 + tid;
+    float m = 0.0f;
+#pragma unroll
+    for (int jj = 0; jj < N; ++jj) m = m + shR[tid * N + jj];
+    const float ep = (t == 0 ? 0.0f : d.ep_acc[sc]) + div_n<N>(m);
+    d.ep_acc[sc] = ep;
+    p.ep_reward[sc] = ep;
+  }
+  // Trainer.train -> ReplayBuffer.sample_batch (rl.py:299-305, 226-241) right after the append
+  // (agent.py:338-342): wave w draws the slots of agent slots 4w .. 4w + 3, two per pass
+  if (p.mode == 0 && d.fused_sample) {
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int j0 = 4 * w + 2 * pass, j1 = j0 + 1;
+      const bool v0 = j0 < AG && s0 + j0 / N < p.S, v1 = j1 < AG && s0 + j1 / N < p.S;
+      sample_slots2(d, s0 * N + j0, s0 * N + j1, v0, v1, l, v0 ? shN[j0] : kB, v1 ? shN[j1] : kB);
+    }
+  }
+}
+
 // ----------------------------------------------------------------- train: Trainer._train
 __device__ __forceinline__ void adam_update(const DqnParams& d, float* th, float* tg, float* mm, float* vv, int idx,
                                             float g, float lr) {
@@ -411,6 +708,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   // (unconditional loads at clamped in-range indices: a branch around them would leave a
   // loop-carried register copy that waits for every load in flight)
   const int a_last = (int)A - 1;
+  const int tag4 = reduce4_tag();
   int slot_n = batch_slot(d, min((int)(blockIdx.x * d.apb) + 1, a_last), threadIdx.x);
   __syncthreads();
 
@@ -435,29 +733,36 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     // ---- layer 1 (K = 5 padded to 8): Z1 = X W1 + b1, 6 target + 2 online row tiles
     const float bt0 = W.bt0, bo0 = W.bo0, bt1 = W.bt1, bo1 = W.bo1, b1t = W.b1t, b1o = W.b1o;
     unsigned z1mask = 0;  // online rows where z1 > 0 (ReLU derivative), bit 4 rt + r
+    // all 16 products first (8 independent accumulators), then the bias / ReLU / LDS stores: no
+    // store waits on the MFMA it follows
+    f32x4 z1[8];
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt) {
-      const int row = 16 * rt + c16, act = row / kB, b = row % kB;
-      const float av = act == 0 ? 0.0f : (act == 1 ? 0.5f : 1.0f);
-      f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      acc = mfma4(smp[b][6 + g4], bt0, acc);
-      acc = mfma4(g4 == 0 ? av : 0.0f, bt1, acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) H1t[16 * rt + 4 * g4 + r][col] = relu(acc[r] + b1t);
+      const int b = (16 * rt + c16) % kB;
+      z1[rt] = mfma4(smp[b][6 + g4], bt0, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
     }
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const int b = 16 * rt + c16;
-      f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      acc = mfma4(smp[b][g4], bo0, acc);
-      acc = mfma4(g4 == 0 ? smp[b][4] : 0.0f, bo1, acc);
+    for (int rt = 0; rt < 2; ++rt) z1[6 + rt] = mfma4(smp[16 * rt + c16][g4], bo0, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+#pragma unroll
+    for (int rt = 0; rt < 6; ++rt) {
+      const int row = 16 * rt + c16, act = row / kB;
+      const float av = act == 0 ? 0.0f : (act == 1 ? 0.5f : 1.0f);
+      z1[rt] = mfma4(g4 == 0 ? av : 0.0f, bt1, z1[rt]);
+    }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) z1[6 + rt] = mfma4(g4 == 0 ? smp[16 * rt + c16][4] : 0.0f, bo1, z1[6 + rt]);
+#pragma unroll
+    for (int rt = 0; rt < 6; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) H1t[16 * rt + 4 * g4 + r][col] = relu(z1[rt][r] + b1t);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float z = acc[r] + b1o;
+        const float z = z1[6 + rt][r] + b1o;
         H1o[16 * rt + 4 * g4 + r][col] = relu(z);
         if (z > 0.0f) z1mask |= 1u << (4 * rt + r);
       }
-    }
     DQN_STAMP(0);
     __syncthreads();
     DQN_STAMP(1);
@@ -481,30 +786,33 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       ao[1] = mfma4(bo, H1o[16 + c16][k], ao[1]);
     }
     DQN_STAMP(2);
-    // ---- layer 3, this wave's 16 units: in-lane over r, then over the 4 row groups (g4)
+    // ---- layer 3, this wave's 16 units: in-lane over r (a pairwise tree), then over the 4 row
+    // groups for four tiles at once (reduce4_groups: 3 lane swaps + 3 adds, row group g4 ends with
+    // tile tag4's sum), so every lane stores one value per four tiles, without a masked branch
+    float s8[8];
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt) {
-      float s = 0.0f;
+      float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) s = s + relu(at[rt][r] + W.b2t[r]) * W.w3t[r];
-      s = sum_groups(s);
-      if (g4 == 0) qpart[w][16 * rt + c16] = s;
+      for (int r = 0; r < 4; ++r) v[r] = relu(at[rt][r] + W.b2t[r]) * W.w3t[r];
+      s8[rt] = (v[0] + v[1]) + (v[2] + v[3]);
     }
     float h2o[2][4];
     unsigned z2mask = 0;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
-      float s = 0.0f;
+      float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float z = ao[rt][r] + W.b2o[r];
         h2o[rt][r] = relu(z);
         if (z > 0.0f) z2mask |= 1u << (4 * rt + r);
-        s = s + h2o[rt][r] * W.w3o[r];
+        v[r] = h2o[rt][r] * W.w3o[r];
       }
-      s = sum_groups(s);
-      if (g4 == 0) qpart[w][3 * kB + 16 * rt + c16] = s;
+      s8[6 + rt] = (v[0] + v[1]) + (v[2] + v[3]);
     }
+    qpart[w][16 * tag4 + c16] = reduce4_groups(s8[0], s8[1], s8[2], s8[3]);
+    qpart[w][4 * kB / 2 + 16 * tag4 + c16] = reduce4_groups(s8[4], s8[5], s8[6], s8[7]);
     DQN_STAMP(3);
     __syncthreads();
     DQN_STAMP(1);
@@ -734,6 +1042,22 @@ __global__ void dqn_forward_kernel(const float* __restrict__ th, int n, const fl
 }  // namespace
 
 hipError_t launch_dqn_act(const DqnParams& d, hipStream_t st) {
+  if (d.n_nets == 1 && !d.act_wave) {  // one shared network: 16 agents per workgroup on MFMA tiles
+    switch (d.e.N) {
+#define P2PMG_DQN_ACT_SHARED(NN)                                                                               \
+  case NN: {                                                                                                   \
+    constexpr int spw = kActAgents / NN;                                                                       \
+    hipLaunchKernelGGL(dqn_act_shared_kernel<NN>, dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d);         \
+    break;                                                                                                     \
+  }
+      P2PMG_DQN_ACT_SHARED(1) P2PMG_DQN_ACT_SHARED(2) P2PMG_DQN_ACT_SHARED(3) P2PMG_DQN_ACT_SHARED(4)
+      P2PMG_DQN_ACT_SHARED(5) P2PMG_DQN_ACT_SHARED(6) P2PMG_DQN_ACT_SHARED(7) P2PMG_DQN_ACT_SHARED(8)
+      P2PMG_DQN_ACT_SHARED(16)
+#undef P2PMG_DQN_ACT_SHARED
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   const dim3 grid(d.e.S);
   switch (d.e.N) {
 #define P2PMG_DQN_ACT(NN) \

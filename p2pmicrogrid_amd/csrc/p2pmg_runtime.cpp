@@ -1555,6 +1555,12 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     for (auto& ev : c->ring) HIP_TRY(c, hipEventCreate(&ev));
   }
   d.fused_sample = (mode == P2PMG_MODE_TRAIN) ? 1 : 0;  // the act launch of each env step draws the samples
+  {  // P2PMG_DQN_ACT=wave: the one-wave-per-agent act kernel for a shared network too (tests, A/B)
+    const char* v = getenv("P2PMG_DQN_ACT");
+    d.act_wave = (v && !strcmp(v, "wave")) ? 1 : 0;
+  }
+  c->last_kernel = std::string(c->n_nets == 1 && !d.act_wave ? "dqn_act_shared_kernel<" : "dqn_act_kernel<") +
+                   std::to_string(c->N) + ">";
   const bool same = mode != P2PMG_MODE_TRAIN || dqn_steps_same(c);
   if (!same) {
     rc = dqn_upload_lr_table(c);

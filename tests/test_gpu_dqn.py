@@ -266,3 +266,44 @@ def test_replay_samples_past_eviction_match_reference_fixture():
     assert n == added0 + T and len(rows) == 5000
     assert np.array_equal(rows, buf[0][(n - 5000 + np.arange(5000)) % 5000])
     eng.close()
+
+
+@pytest.mark.parametrize("S,N,R", [(37, 2, 1), (11, 3, 2), (5, 16, 1), (20, 1, 0), (9, 5, 1)])
+def test_shared_act_mfma_kernel_equals_wave_kernel(S, N, R, monkeypatch):
+    """A shared network's act launch on MFMA tiles (dqn_act_shared_kernel, 16 agents per workgroup,
+    partial last workgroup when 16 / N does not divide S) gives bitwise the records, replay rings,
+    sampled slots and trained weights of the one-wave-per-agent kernel (P2PMG_DQN_ACT=wave): same
+    fmaf chain over k in layer 2, same pairwise tree over the 64 units in layer 3."""
+    T = 24
+    runs = []
+    for kind in ("wave", "mfma"):
+        if kind == "wave":
+            monkeypatch.setenv("P2PMG_DQN_ACT", "wave")
+        else:
+            monkeypatch.delenv("P2PMG_DQN_ACT", raising=False)
+        inp = scenario_batch(S, N, T)
+        eng = DeviceDQNBatch(S, N, R, T, shared=True, init_seed=11)
+        eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+        eng.set_profiles(inp.load_w, inp.pv_w)
+        eng.set_max_in(inp.max_in)
+        eng.set_temperatures(inp.t_in0, inp.t_m0)
+        recs = []
+        keys = ("reward", "cost", "grid", "p2p", "t_in", "action")
+        for ep, (mode, eps) in enumerate((("fill", 1.0), ("fill", 1.0), ("train", 0.6), ("train", 0.2))):
+            eng.run_episode(mode, "philox", episode=ep, epsilon=eps, record=keys + (("loss",) if mode == "train" else ()))
+            assert eng.last_kernel().startswith("dqn_act_kernel<" if kind == "wave" else "dqn_act_shared_kernel<")
+            recs.append(eng.get_records(list(keys) + (["loss"] if mode == "train" else [])))
+            recs.append({"episode_reward": eng.episode_reward()})
+            eng.reset_temperatures_philox(ep + 1)
+        eng.run_episode("greedy", record=keys)
+        recs.append(eng.get_records(list(keys)))
+        buf, added = eng.get_buffer()
+        runs.append((recs, buf, added, eng.get_weights("online"), eng.get_weights("target")))
+        eng.close()
+    (ra, ba, aa, tha, tga), (rb, bb, ab, thb, tgb) = runs
+    for x, y in zip(ra, rb):
+        for k in x:
+            assert np.array_equal(np.asarray(x[k]), np.asarray(y[k]), equal_nan=True), k
+    assert np.array_equal(aa, ab)
+    assert np.array_equal(ba, bb)
+    assert np.array_equal(tha, thb) and np.array_equal(tga, tgb)
