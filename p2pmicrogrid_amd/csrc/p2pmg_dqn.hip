@@ -27,6 +27,7 @@ namespace {
 constexpr int kH = 64;
 constexpr int kB = kDqnBatch;
 constexpr int kLdsRow = 68;  // padded activation rows: an MFMA A-operand read (16 rows x 4 k) hits 64 banks
+constexpr int kLdsRowT = 48;  // H1oT rows (32 data rows + pad): 16 units x 4 k of one read hit 64 banks
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -661,7 +662,7 @@ template <bool SHARED>
 __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) {  // 2 waves / SIMD
   __shared__ float smpb[2][kB * kTrans];  // this agent's batch and the next one's (prefetched)
   __shared__ float H1t[3 * kB][kLdsRow];
-  __shared__ float H1o[kB][kLdsRow];
+  __shared__ __attribute__((aligned(16))) float H1oT[kH][kLdsRowT];  // online layer-1 activations, unit-major
   __shared__ __attribute__((aligned(16))) float dZ2[kB][kLdsRow];
   __shared__ float qpart[4][4 * kB];  // per-wave partial Q: rows 0..95 target (action x sample), 96..127 online
   const EpisodeParams& p = d.e;
@@ -669,12 +670,13 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   const int c16 = l & 15, g4 = l >> 4;
   const int col = 16 * w + c16;     // this lane's column of layer 1 and of dH1
   const int h0 = 16 * w + 4 * g4;   // this lane's 4 hidden units of layer 2 (transposed tiles)
+  const int xc = c16 < 5 ? c16 : 4;  // dW1: this lane's input feature
   const size_t A = (size_t)p.A;
 
-  f32x4 gW2[4], gW1;
+  f32x4 gW2[4], gW1[2];
 #pragma unroll
   for (int m = 0; m < 4; ++m) gW2[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  gW1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  gW1[0] = gW1[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   float gb1 = 0.0f, gb3 = 0.0f;
   float gb2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gW3[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   const int n_ag = d.batch ? 1 : d.apb;
@@ -691,7 +693,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     for (int kk = 0; kk < 16; ++kk) {
       w2t[kk] = tg0[kOffW2 + (4 * kk + g4) * kH + col];
       w2o[kk] = th0[kOffW2 + (4 * kk + g4) * kH + col];
-      w2c[kk] = th0[kOffW2 + col * kH + 4 * kk + g4];
+      w2c[kk] = th0[kOffW2 + col * kH + 16 * g4 + kk];  // dH1's K order: unit 16 g4 + kk
     }
   }
   // the first agent's batch (explicit batch, or the sample pre-pass output)
@@ -756,13 +758,16 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
 #pragma unroll
       for (int r = 0; r < 4; ++r) H1t[16 * rt + 4 * g4 + r][col] = relu(z1[rt][r] + b1t);
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < 2; ++rt) {
+      float h[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float z = z1[6 + rt][r] + b1o;
-        H1o[16 * rt + 4 * g4 + r][col] = relu(z);
+        h[r] = relu(z);
         if (z > 0.0f) z1mask |= 1u << (4 * rt + r);
       }
+      *reinterpret_cast<float4*>(&H1oT[col][16 * rt + 4 * g4]) = make_float4(h[0], h[1], h[2], h[3]);
+    }
     DQN_STAMP(0);
     __syncthreads();
     DQN_STAMP(1);
@@ -782,8 +787,8 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       const float bo = SHARED ? w2o[SHARED ? kk : 0] : th[kOffW2 + k * kH + col];
 #pragma unroll
       for (int rt = 0; rt < 6; ++rt) at[rt] = mfma4(bt, H1t[16 * rt + c16][k], at[rt]);
-      ao[0] = mfma4(bo, H1o[c16][k], ao[0]);
-      ao[1] = mfma4(bo, H1o[16 + c16][k], ao[1]);
+      ao[0] = mfma4(bo, H1oT[k][c16], ao[0]);
+      ao[1] = mfma4(bo, H1oT[k][16 + c16], ao[1]);
     }
     DQN_STAMP(2);
     // ---- layer 3, this wave's 16 units: in-lane over r (a pairwise tree), then over the 4 row
@@ -868,35 +873,60 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     DQN_STAMP(4);
     __syncthreads();
     DQN_STAMP(1);
-    // dW2 = H1^T dZ2 (K = the 32 data rows), accumulator rows = layer-1 units 16 mt + 4 g4 + r,
+    // Every operand of the backward products is read from LDS up front (16-B reads where the K
+    // order allows), so the MFMA chains below never wait on a read between two products.
+    // dW2 = H1^T dZ2 over the 32 data rows in the K order b = 8 g4 + q: A = H1oT[16 mt + c16][b]
+    // (two 16-B reads per mt), B = dZ2[b][col]; accumulator rows = layer-1 units 16 mt + 4 g4 + r,
     // columns = the wave's layer-2 units col
+    float ha[4][8], db[8];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const float4 u0 = *reinterpret_cast<const float4*>(&H1oT[16 * mt + c16][8 * g4]);
+      const float4 u1 = *reinterpret_cast<const float4*>(&H1oT[16 * mt + c16][8 * g4 + 4]);
+      ha[mt][0] = u0.x; ha[mt][1] = u0.y; ha[mt][2] = u0.z; ha[mt][3] = u0.w;
+      ha[mt][4] = u1.x; ha[mt][5] = u1.y; ha[mt][6] = u1.z; ha[mt][7] = u1.w;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) db[q] = dZ2[8 * g4 + q][col];
+    // dH1 = dZ2 W2^T (own columns n = col) in the K order unit 16 g4 + kk: A = dZ2[16 rt + c16][16 g4
+    // .. + 15] (four 16-B reads per rt), B = W2[col][16 g4 + kk] (registers for a shared network)
+    float za[2][16];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float4 u = *reinterpret_cast<const float4*>(&dZ2[16 * rt + c16][16 * g4 + 4 * v]);
+        za[rt][4 * v] = u.x; za[rt][4 * v + 1] = u.y; za[rt][4 * v + 2] = u.z; za[rt][4 * v + 3] = u.w;
+      }
+    // dW1's A operand: input feature c16 (< 5) of data rows b = 16 rt + 4 g4 + r (lanes c16 >= 5 read
+    // feature 4 and select 0: no exec-masked read)
+    float xa[2][4];
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int b = 16 * rt + 4 * g4 + r;
-        const float dzb = dZ2[b][col];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) gW2[mt] = mfma4(H1o[b][16 * mt + c16], dzb, gW2[mt]);
-      }
-    // dH1 = dZ2 W2^T (own columns m = col), then dZ1 = dH1 * [z1 > 0]; dW1 = X^T dZ1
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const int j = 4 * kk + g4;
-        acc = mfma4(dZ2[16 * rt + c16][j], SHARED ? w2c[SHARED ? kk : 0] : th[kOffW2 + col * kH + j], acc);
+        const float x = smp[16 * rt + 4 * g4 + r][xc];
+        xa[rt][r] = c16 < 5 ? x : 0.0f;
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = 16 * rt + 4 * g4 + r;
-        const float dz1 = ((z1mask >> (4 * rt + r)) & 1u) ? acc[r] : 0.0f;
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) gW2[mt] = mfma4(ha[mt][q], db[q], gW2[mt]);
+    f32x4 acc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+        acc[rt] = mfma4(za[rt][kk], SHARED ? w2c[SHARED ? kk : 0] : th[kOffW2 + col * kH + 16 * g4 + kk], acc[rt]);
+    // dZ1 = dH1 * [z1 > 0]; dW1 = X^T dZ1 (two accumulators: independent chains)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const float dz1 = ((z1mask >> (4 * rt + r)) & 1u) ? acc[rt][r] : 0.0f;
         gb1 += dz1;
-        const float x = c16 < 5 ? smp[b][c16] : 0.0f;
-        gW1 = mfma4(x, dz1, gW1);
+        gW1[rt] = mfma4(xa[rt][r], dz1, gW1[rt]);
       }
-    }
     if (has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
     DQN_STAMP(5);
     __syncthreads();  // every wave is done with this agent's LDS and with the online W2
@@ -932,7 +962,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int k = 4 * g4 + r;
-      if (k < 5) adam_update(d, th, tg, mm, vv, kOffW1 + k * kH + col, fminf(fmaxf(gW1[r], -d.clip), d.clip), lr);
+      if (k < 5) adam_update(d, th, tg, mm, vv, kOffW1 + k * kH + col, fminf(fmaxf(gW1[0][r] + gW1[1][r], -d.clip), d.clip), lr);
     }
     if (g4 == 0) adam_update(d, th, tg, mm, vv, kOffB1 + col, gb1, lr);
     if (c16 == 0) {
@@ -951,7 +981,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       for (int r = 0; r < 4; ++r) gp[kOffW2 + (16 * mt + 4 * g4 + r) * kH + col] = gW2[mt][r];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (4 * g4 + r < 5) gp[kOffW1 + (4 * g4 + r) * kH + col] = gW1[r];
+      if (4 * g4 + r < 5) gp[kOffW1 + (4 * g4 + r) * kH + col] = gW1[0][r] + gW1[1][r];
     if (g4 == 0) gp[kOffB1 + col] = gb1;
     if (c16 == 0) {
 #pragma unroll
