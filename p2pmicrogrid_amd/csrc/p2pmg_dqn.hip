@@ -315,49 +315,40 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
 constexpr int kActAgents = 16;
 constexpr int kActRows = 3 * kActAgents;  // row = action * 16 + agent slot
 
-// ReplayBuffer.sample_batch (rl.py:226-241) for two agents in one wave: lanes 0..31 draw agent a0's
-// 32 slots, lanes 32..63 agent a1's (sample_slots's Floyd loop with half-wave ballots)
-__device__ __forceinline__ void sample_slots2(const DqnParams& d, int a0, int a1, bool v0, bool v1, int l, int n0,
-                                              int n1) {
-  const EpisodeParams& p = d.e;
-  const size_t A = (size_t)p.A;
-  const bool hi = l >= 32;
-  const int jl = l & 31;
-  const int a = hi ? a1 : a0;
-  const int n_added = hi ? n1 : n0;
-  const int count = n_added < d.cap ? n_added : d.cap;
-  const int first = n_added - count;
-  int idx = 0;
-  if (d.samples) {
-    idx = (hi ? v1 : v0) ? (int)d.samples[((size_t)d.t * A + a) * kB + jl] : 0;
-  } else {
-    uint32_t c0 = (uint32_t)d.t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a, c3 = kTagSample + (uint32_t)jl;
-    philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-    const int mj = count - kB + jl;
-    const int rj = (int)__umulhi(c0, (uint32_t)(mj + 1));
-    idx = rj;
-    for (int j = 0; j < kB; ++j) {
-      const int rlo = __builtin_amdgcn_readlane(rj, j), rhi = __builtin_amdgcn_readlane(rj, j + 32);
-      const int r = hi ? rhi : rlo;
-      const uint64_t m = __ballot(jl < j && idx == r);
-      const bool taken = hi ? (m >> 32) != 0 : (uint32_t)m != 0;
-      if (jl == j) idx = taken ? count - kB + j : r;
-    }
-  }
-  if (hi ? v1 : v0) reinterpret_cast<int*>(d.smp)[(size_t)a * kB + jl] = (first + idx) % d.cap;
-}
-
+#ifndef P2PMG_TRACE
+#define P2PMG_TRACE 0
+#endif
+#if P2PMG_TRACE  // timing-only: s_memtime phase splits of wave 0 (scripts/gpu_dqn_trace.sh)
+#define ACT_STAMP(k)                                                             \
+  do {                                                                           \
+    uint64_t t_;                                                                 \
+    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    atr[k] += t_ - alast;                                                        \
+    alast = t_;                                                                  \
+  } while (0)
+#else
+#define ACT_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
 template <int N>
 __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) {
   constexpr int SPW = kActAgents / N;  // scenarios per workgroup
   constexpr int AG = SPW * N;          // agents per workgroup (<= 16)
   const EpisodeParams& p = d.e;
+#if P2PMG_TRACE
+  uint64_t atr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, alast;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(alast)::"memory");
+#endif
   __shared__ float shP[2][AG * N];
   __shared__ float4 shX[kActAgents];   // time, normalised T_in, balance, p2p of agent slot j
   __shared__ float H1[kActRows][kLdsRow];
   __shared__ float qpart[4][kActRows + 16];  // + the 4th (unused) tile of reduce4_groups
   __shared__ float shR[AG];
   __shared__ int shN[kActAgents];
+  __shared__ float shEp[kActAgents];
+  __shared__ int shFlag[2];
+  __shared__ __attribute__((aligned(16))) int shI[kActAgents][kB];  // Floyd draws of the replay sample
   const int tid = threadIdx.x;
   const int w = tid / kWave, l = tid % kWave;
   const int c16 = l & 15, g4 = l >> 4;
@@ -377,12 +368,16 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
   const int s_env = p.n_env == 1 ? 0 : (agent_thr ? s : 0);
   const float* e0 = p.env + ((size_t)t * p.n_env + s_env) * kEnvStride;
   const float* e1 = p.env + ((size_t)tn * p.n_env + s_env) * kEnvStride;
+  float buy = 0.0f, inj = 0.0f, p2pp = 0.0f;
   float time_t = 0.0f, t_out = 0.0f, time_n = 0.0f, mi = 1.0f, tin = 0.0f, tm = 0.0f, bal = 0.0f, baln = 0.0f,
         tnorm = 0.0f;
   float4 lv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (agent_thr) {
     time_t = e0[0];
     t_out = e0[1];
+    buy = e0[2];
+    inj = e0[3];
+    p2pp = e0[4];
     time_n = e1[0];
     const float2 f0 = p.prof[(size_t)t * A + a], f1 = p.prof[(size_t)tn * A + a];
     mi = p.max_in[a];
@@ -393,6 +388,10 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
     tnorm = (tin - p.setpoint) / p.margin;  // HPHeating.normalized_temperature heating.py:118-120
     lv = p.hp_lv[a];
   }
+  // loaded with the inputs: a load issued after the step's stores would wait for their completion
+  // (vmcnt counts loads and stores in issue order)
+  const int32_t n_added = (agent_thr && p.mode != 1) ? d.added[a] : 0;
+  const float ep_prev = (tid < SPW && s0 + tid < p.S && t != 0) ? d.ep_acc[s0 + tid] : 0.0f;
   // layer 1 (thread = hidden unit u of agent slots 4 * (tid / 64) .. + 3): W1 column and b1
   const int u = l;
   const float w10 = th[kOffW1 + 0 * kH + u], w11 = th[kOffW1 + 1 * kH + u], w12 = th[kOffW1 + 2 * kH + u],
@@ -411,9 +410,14 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
   const int tag4 = reduce4_tag();
 
   if (tid < AG * N) shP[0][tid] = 0.0f;
+  // consumed here, before the rounds' record stores: a later first use would wait for those stores
+  if (agent_thr) shN[j] = n_added + 1;
+  if (tid < SPW) shEp[tid] = ep_prev;
   __syncthreads();
+  ACT_STAMP(0);
   int cur = 0, act = 0, code = 255;
   float hp = 0.0f, p2pf = 0.0f;
+  uint64_t act_pack = 0;
   for (int r = 0; r < R1; ++r) {
     const float* P = shP[cur] + sl * N * N;  // this agent's scenario
     bool greedy = false;
@@ -438,6 +442,7 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
       greedy = code == 255;
       shX[j] = make_float4(time_t, tnorm, bal, p2pf);
     }
+    ACT_STAMP(1);
     if (__syncthreads_or(greedy)) {
       // layer 1: the three action rows of agent slots 4 (tid / 64) .. + 3 at unit u
 #pragma unroll
@@ -471,6 +476,7 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
       qpart[w][16 * tag4 + c16] = reduce4_groups(sq[0], sq[1], sq[2], 0.0f);  // ... the 4 row groups
       __syncthreads();
     }
+    ACT_STAMP(2);
     if (agent_thr) {
       if (greedy) {
         // ActorModel.greedy_action rl.py:188-196: Q(obs, a) for a in (0, .5, 1), argmax (first max)
@@ -508,15 +514,21 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
         else v = (jj == i) ? (tot == tot ? out * 0.0f : tot) : (out * fabsf(f[jj])) / tot;
         Pn[jj] = v;
       }
-      if (p.record & 32) p.rec_action[((size_t)t * R1 + r) * A + a] = (uint8_t)act;
+      if (p.record & 32) {  // stored with the other records at the end (up to 8 rounds)
+        if (R1 <= 8) act_pack |= (uint64_t)act << (8 * r);
+        else p.rec_action[((size_t)t * R1 + r) * A + a] = (uint8_t)act;
+      }
     }
     __syncthreads();
     cur ^= 1;
+    ACT_STAMP(3);
   }
+  // the step's stores all go out at the end of the kernel, after the replay draws: nothing after them
+  // waits on vmcnt (which counts stores and loads alike)
+  float g = 0.0f, pp = 0.0f, cost = 0.0f, rw = 0.0f, tin0 = tin;
   if (agent_thr) {
     // CommunityMicrogrid._assign_powers community.py:45-54 (final P, diagonal kept)
     const float* P = shP[cur] + sl * N * N;
-    float g = 0.0f, pp = 0.0f;
 #pragma unroll
     for (int jj = 0; jj < N; ++jj) {
       const float pij = P[i * N + jj], pji = P[jj * N + i];
@@ -525,17 +537,95 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
       pp = pp + ex;
     }
     // _compute_costs community.py:56-65; RLAgent.get_reward agent.py:225-232 (pre-update T_in)
-    const float buy = e0[2], inj = e0[3], p2pp = e0[4];
-    float cost = (g >= 0.0f) ? g * buy : g * inj;
+    cost = (g >= 0.0f) ? g * buy : g * inj;
     cost = cost + pp * p2pp;
     cost = (cost * p.slot) / p.mph;
     cost = cost * p.kilo;
     float pen = fmaxf(fmaxf(0.0f, p.lower - tin), fmaxf(0.0f, tin - p.upper));
     pen = pen > 0.0f ? pen + 1.0f : 0.0f;
-    const float rw = -(cost + p.penw * pen);
+    rw = -(cost + p.penw * pen);
+    rc_update(p, t_out, hp, tin, tm);  // HPHeating.step heating.py:138-143
+    shR[j] = rw;
+  }
+  __syncthreads();
+  ACT_STAMP(4);
+  float ep = 0.0f;
+  if (tid < SPW) {  // avg_reward = sum_t mean_i r (community.py:179), canonical order
+    float m = 0.0f;
+#pragma unroll
+    for (int jj = 0; jj < N; ++jj) m = m + shR[tid * N + jj];
+    ep = shEp[tid] + div_n<N>(m);
+  }
+  // Trainer.train -> ReplayBuffer.sample_batch (rl.py:299-305, 226-241) right after the append
+  // (agent.py:338-342).  Floyd's draw j keeps r_j unless an earlier draw l < j ended on r_j, when it
+  // takes count - 32 + j.  Sixteen threads per agent (draws q and q + 16) solve that recurrence as a
+  // fixpoint over the agent's 32 indices in LDS: every pass recomputes each draw from the current
+  // indices of the earlier ones, so after pass k the first k draws are final and a pass that changes
+  // nothing has reached the sequential result (typically 2 passes instead of 32 serial steps).
+  if (p.mode == 0 && d.fused_sample) {
+    const int aj = tid >> 4, q0 = tid & 15, q1 = q0 + 16;
+    const bool va = aj < AG && s0 + aj / N < p.S;
+    const int a2 = va ? s0 * N + aj : 0;
+    const int n_add = va ? shN[aj] : kB;
+    const int count = n_add < d.cap ? n_add : d.cap;
+    const int fm = (n_add - count) % d.cap;  // ring slot of the deque's first element
+    int i0, i1;
+    if (d.samples) {
+      i0 = va ? (int)d.samples[((size_t)t * A + a2) * kB + q0] : 0;
+      i1 = va ? (int)d.samples[((size_t)t * A + a2) * kB + q1] : 0;
+    } else {
+      int r[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = h ? q1 : q0;
+        uint32_t c0 = (uint32_t)t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a2, c3 = kTagSample + (uint32_t)q;
+        philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
+        r[h] = (int)__umulhi(c0, (uint32_t)(count - kB + q + 1));
+      }
+      i0 = r[0];
+      i1 = r[1];
+      shI[aj][q0] = i0;
+      shI[aj][q1] = i1;
+      if (tid == 0) shFlag[0] = 0;
+      __syncthreads();
+      // branch-free pass: bit l of hit_h says draw l's current index equals r_h; only l < q counts
+      const uint32_t early0 = (1u << q0) - 1u, early1 = (q1 == 31 ? 0x7FFFFFFFu : (1u << q1) - 1u);
+      for (int pass = 0;; ++pass) {
+        uint32_t hit0 = 0u, hit1 = 0u;
+#pragma unroll
+        for (int v = 0; v < kB / 4; ++v) {
+          const int4 x = *reinterpret_cast<const int4*>(&shI[aj][4 * v]);
+          const int xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            hit0 |= xs[e] == r[0] ? 1u << (4 * v + e) : 0u;
+            hit1 |= xs[e] == r[1] ? 1u << (4 * v + e) : 0u;
+          }
+        }
+        const int n0 = (hit0 & early0) ? count - kB + q0 : r[0], n1 = (hit1 & early1) ? count - kB + q1 : r[1];
+        const bool ch = n0 != i0 || n1 != i1;
+        __syncthreads();  // every read of this pass before any write
+        i0 = n0;
+        i1 = n1;
+        shI[aj][q0] = i0;
+        shI[aj][q1] = i1;
+        if (ch) shFlag[pass & 1] = 1;
+        if (tid == 0) shFlag[(pass + 1) & 1] = 0;
+        __syncthreads();
+        if (shFlag[pass & 1] == 0) break;  // workgroup-uniform: nothing changed in this pass
+      }
+    }
+    if (va) {
+      int* out = reinterpret_cast<int*>(d.smp) + (size_t)a2 * kB;
+      const int sl0 = fm + i0, sl1 = fm + i1;
+      out[q0] = sl0 >= d.cap ? sl0 - d.cap : sl0;
+      out[q1] = sl1 >= d.cap ? sl1 - d.cap : sl1;
+    }
+  }
+  if (agent_thr) {
     if (p.mode != 1) {
       // DQNAgent.save_memory agent.py:332-336 -> ReplayBuffer.add rl.py:208-212
-      const int32_t n_added = d.added[a];
+      const int n_added = shN[j] - 1;
       float2* slot = reinterpret_cast<float2*>(d.buf + ((size_t)a * d.cap + (size_t)(n_added % d.cap)) * kTrans);
       const float av = act == 0 ? 0.0f : (act == 1 ? 0.5f : 1.0f);
       slot[0] = make_float2(time_t, tnorm);
@@ -544,39 +634,30 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
       slot[3] = make_float2(time_n, tnorm);  // next state: same (pre-update) temperature (community.py:161)
       slot[4] = make_float2(baln, 0.0f / mi);  // next state p2p = mean(zeros) / max_in
       d.added[a] = n_added + 1;
-      shN[j] = n_added + 1;
     }
     const size_t k = (size_t)t * A + a;
     if (p.record & 1) p.rec_reward[k] = rw;
     if (p.record & 2) p.rec_cost[k] = cost;
     if (p.record & 4) p.rec_grid[k] = g;
     if (p.record & 8) p.rec_p2p[k] = pp;
-    if (p.record & 16) p.rec_tin[k] = tin;
-    rc_update(p, t_out, hp, tin, tm);  // HPHeating.step heating.py:138-143
+    if (p.record & 16) p.rec_tin[k] = tin0;
+    if ((p.record & 32) && R1 <= 8)
+      for (int r = 0; r < R1; ++r) p.rec_action[((size_t)t * R1 + r) * A + a] = (uint8_t)(act_pack >> (8 * r));
     p.t_in[a] = tin;
     p.t_m[a] = tm;
-    shR[j] = rw;
   }
-  __syncthreads();
-  if (tid < SPW && s0 + tid < p.S) {  // avg_reward = sum_t mean_i r (community.py:179), canonical order
-    const int sc = s0 + tid;
-    float m = 0.0f;
-#pragma unroll
-    for (int jj = 0; jj < N; ++jj) m = m + shR[tid * N + jj];
-    const float ep = (t == 0 ? 0.0f : d.ep_acc[sc]) + div_n<N>(m);
-    d.ep_acc[sc] = ep;
-    p.ep_reward[sc] = ep;
+  if (tid < SPW && s0 + tid < p.S) {
+    d.ep_acc[s0 + tid] = ep;
+    p.ep_reward[s0 + tid] = ep;
   }
-  // Trainer.train -> ReplayBuffer.sample_batch (rl.py:299-305, 226-241) right after the append
-  // (agent.py:338-342): wave w draws the slots of agent slots 4w .. 4w + 3, two per pass
-  if (p.mode == 0 && d.fused_sample) {
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      const int j0 = 4 * w + 2 * pass, j1 = j0 + 1;
-      const bool v0 = j0 < AG && s0 + j0 / N < p.S, v1 = j1 < AG && s0 + j1 / N < p.S;
-      sample_slots2(d, s0 * N + j0, s0 * N + j1, v0, v1, l, v0 ? shN[j0] : kB, v1 ? shN[j1] : kB);
-    }
-  }
+#if P2PMG_TRACE
+  ACT_STAMP(5);
+  if (l == 0 && w == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2) && (d.t == 50 || d.t == 51))
+    printf("ACTTRACE blk %d t %d mode %d: prologue %llu agentA %llu forward %llu agentB %llu epilogue %llu sample %llu\n",
+           (int)blockIdx.x, d.t, p.mode, (unsigned long long)atr[0], (unsigned long long)atr[1],
+           (unsigned long long)atr[2], (unsigned long long)atr[3], (unsigned long long)atr[4],
+           (unsigned long long)atr[5]);
+#endif
 }
 
 // ----------------------------------------------------------------- train: Trainer._train
