@@ -249,6 +249,16 @@ MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_16x
 DQN_FWD_FLOP = 2 * (5 * 64 + 64 * 64 + 64 * 1)  # QNetwork (rl.py:135-148): 8,960 FLOP per row
 
 
+def collective_record(eng, world: int, steps: int):
+    """The data-path all-reduces of the timed episodes (shared-table delta once per episode, DQN
+    gradient once per env step): HIP-event time on the rank's stream, rank 0's view (world > 1)."""
+    if world <= 1 or not hasattr(eng, "collective_ms"):
+        return None
+    total, n = eng.collective_ms()
+    return {"kind": "RCCL allReduce (data path)", "calls": n, "ms_total": total,
+            "ms_per_step": total / max(steps, 1), "us_per_call": 1e3 * total / n if n else None}
+
+
 def dqn_flop_per_agent_step(R: int) -> int:
     """Trainer._train (rl.py:307-333) = 3 target forwards x 32 samples +
     1 online forward + backward (2x forward) x 32 = 32 * 6 * 8,960; the greedy action choice
@@ -320,6 +330,7 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     rank_times = all_gather_float(time.perf_counter() - t0, world)
     dt = max(rank_times)
     kms = eng.kernel_times()
+    coll = collective_record(eng, world, args.steps)
     steps_per_episode = S * N * T
     flop = dqn_flop_per_agent_step(R)
     episode_ms = float(np.mean(kms)) if len(kms) else float("nan")
@@ -345,6 +356,8 @@ def main_dqn(args, rank, world, local, S, N, R, T):
             "rccl_nranks": eng.comm_nranks() if not comm_err else 0,
             "rank_times_s": rank_times,
         }
+        if coll:
+            out["collective"] = coll
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_dqn(args.cpu_seconds, R=R, T=T)
             out["cpu_baseline"].update(os_cpu_count=os.cpu_count(), threads=1)
@@ -582,6 +595,7 @@ def main():
     rank_times = all_gather_float(time.perf_counter() - t0, world)
     dt = max(rank_times)
     kms = eng.kernel_times()
+    coll = collective_record(eng, world, args.steps)
     ep_reward = metrics[0] / metrics[1]
     nranks = eng.comm_nranks() if not comm_err else 0
     hashes = eng.table_hash_allgather() if shared else None  # every replica of the shared table
@@ -642,6 +656,8 @@ def main():
             out["test_engine"] = os.environ["P2PMG_BENCH_TEST_ENGINE"]
         if comm_err:
             out["rccl_error"] = comm_err
+        if coll:
+            out["collective"] = coll
         if shared:
             out["table_replicas_identical"] = bool(np.all(hashes == hashes[0]))
             assert out["table_replicas_identical"], f"shared-table replicas differ across ranks: {hashes}"

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define P2PMG_ABI_VERSION 4  /* 3: p2pmg_episode_args.next_epsilon; 4: P2PMG_FLAG_NEXT_EPSILON, p2pmg_prepass_stats, per-network Adam steps */
+#define P2PMG_ABI_VERSION 5  /* 3: p2pmg_episode_args.next_epsilon; 4: P2PMG_FLAG_NEXT_EPSILON, p2pmg_prepass_stats, per-network Adam steps; 5: p2pmg_collective_ms */
 
 typedef struct p2pmg_ctx p2pmg_ctx;
 
@@ -201,6 +201,11 @@ int p2pmg_last_kernel_ms(p2pmg_ctx* ctx, float* ms);           /* HIP-event time
  * (ring of the last 4096 launches, on the context's stream); *count = entries written. */
 int p2pmg_kernel_times(p2pmg_ctx* ctx, float* ms, int max, int* count);
 int p2pmg_reset_kernel_times(p2pmg_ctx* ctx);
+/* Sum of the HIP-event durations (ms) of the data-path RCCL all-reduces (shared-table delta,
+ * DQN gradient; not the episode metrics) enqueued since p2pmg_reset_kernel_times, over the last
+ * 1024 of them; *count = all-reduces summed.  No reference counterpart (the reference is one
+ * process); the multi-GPU bench line reports it. */
+int p2pmg_collective_ms(p2pmg_ctx* ctx, double* total_ms, int* count);
 /* Stamp the episode kernel's timing events on every period-th episode launch only (default 1 =
  * every launch; the counter restarts here and at p2pmg_reset_kernel_times, so the next launch is
  * timed).  Timing-only: results do not depend on it. */

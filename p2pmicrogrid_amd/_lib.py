@@ -31,7 +31,7 @@ EXPORTS = [
     "p2pmg_set_replay_codes", "p2pmg_zero_q", "p2pmg_set_q", "p2pmg_get_q", "p2pmg_run_episode",
     "p2pmg_get_record", "p2pmg_get_episode_reward", "p2pmg_last_kernel_ms", "p2pmg_rc_step",
     "p2pmg_state_indices", "p2pmg_replay_decode", "p2pmg_device_count", "p2pmg_kernel_times",
-    "p2pmg_reset_kernel_times", "p2pmg_set_timing_period", "p2pmg_q_calls", "p2pmg_set_hp_levels", "p2pmg_set_battery", "p2pmg_get_soc",
+    "p2pmg_reset_kernel_times", "p2pmg_collective_ms", "p2pmg_set_timing_period", "p2pmg_q_calls", "p2pmg_set_hp_levels", "p2pmg_set_battery", "p2pmg_get_soc",
     "p2pmg_battery_seq", "p2pmg_apply_q_delta", "p2pmg_get_q_delta", "p2pmg_set_q_delta", "p2pmg_comm_unique_id", "p2pmg_comm_init",
     "p2pmg_allreduce_q_delta", "p2pmg_comm_destroy", "p2pmg_run_rule_episode", "p2pmg_set_hp_state",
     "p2pmg_get_hp_state",
@@ -64,7 +64,7 @@ class DqnConfig(C.Structure):
                 ("capacity", C.c_int32), ("agents_per_block", C.c_int32), ("reserved", C.c_int32)]
 
 
-ABI_VERSION = 4  # include/p2pmg.h P2PMG_ABI_VERSION
+ABI_VERSION = 5  # include/p2pmg.h P2PMG_ABI_VERSION
 
 
 class EpisodeArgs(C.Structure):
@@ -117,6 +117,7 @@ def _declare(lib):
         "p2pmg_device_count": ([C.POINTER(C.c_int)], i32),
         "p2pmg_kernel_times": ([vp, fp, i32, C.POINTER(C.c_int)], i32),
         "p2pmg_reset_kernel_times": ([vp], i32),
+        "p2pmg_collective_ms": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_int)], i32),
         "p2pmg_set_timing_period": ([vp, i32], i32),
         "p2pmg_q_calls": ([vp, i32, vp, vp, vp, vp, vp, i32, vp, vp], i32),
         "p2pmg_set_hp_levels": ([vp, fp], i32),

@@ -777,6 +777,11 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       w2c[kk] = th0[kOffW2 + col * kH + 16 * g4 + kk];  // dH1's K order: unit 16 g4 + kk
     }
   }
+#ifdef P2PMG_TRAIN_SKEW  // timing experiment: the second half of the grid starts later
+  if (blockIdx.x >= gridDim.x / 2) {
+    for (int k = 0; k < P2PMG_TRAIN_SKEW; ++k) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
   // the first agent's batch (explicit batch, or the sample pre-pass output)
   if (d.batch) {
     for (int k = threadIdx.x; k < kB * kTrans; k += 256) smpb[0][k] = d.batch[k];
@@ -853,6 +858,9 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     __syncthreads();
     DQN_STAMP(1);
 
+#ifdef P2PMG_TRAIN_PRIO
+    __builtin_amdgcn_s_setprio(2);
+#endif
     // ---- layer 2 as Z2^T = W2^T H1^T (K = 64): the operands of H1 W2 with the MFMA's A and B
     // swapped, so the accumulator of row tile rt holds data row 16 rt + c16 at the hidden units
     // h0 + r.  Layer 3 then sums 4 units in-lane and the 4 row groups with two exchanges, instead
@@ -871,6 +879,9 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       ao[0] = mfma4(bo, H1oT[k][c16], ao[0]);
       ao[1] = mfma4(bo, H1oT[k][16 + c16], ao[1]);
     }
+#ifdef P2PMG_TRAIN_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     DQN_STAMP(2);
     // ---- layer 3, this wave's 16 units: in-lane over r (a pairwise tree), then over the 4 row
     // groups for four tiles at once (reduce4_groups: 3 lane swaps + 3 adds, row group g4 ends with
@@ -954,6 +965,9 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     DQN_STAMP(4);
     __syncthreads();
     DQN_STAMP(1);
+#ifdef P2PMG_TRAIN_PRIO
+    __builtin_amdgcn_s_setprio(2);
+#endif
     // Every operand of the backward products is read from LDS up front (16-B reads where the K
     // order allows), so the MFMA chains below never wait on a read between two products.
     // dW2 = H1^T dZ2 over the 32 data rows in the K order b = 8 g4 + q: A = H1oT[16 mt + c16][b]
@@ -1008,6 +1022,9 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
         gb1 += dz1;
         gW1[rt] = mfma4(xa[rt][r], dz1, gW1[rt]);
       }
+#ifdef P2PMG_TRAIN_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if (has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
     DQN_STAMP(5);
     __syncthreads();  // every wave is done with this agent's LDS and with the online W2

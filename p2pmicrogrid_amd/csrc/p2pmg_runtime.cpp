@@ -36,6 +36,9 @@ struct p2pmg_ctx {
   static constexpr int kRing = 4096;
   std::vector<hipEvent_t> ring;  // 2 * kRing events: start/stop of each episode kernel
   long long n_timed = 0;          // launches recorded since the last reset
+  static constexpr int kCRing = 1024;
+  std::vector<hipEvent_t> cring;  // 2 * kCRing events: start/stop of each data-path RCCL all-reduce
+  long long n_coll = 0;           // collectives recorded since the last reset
   int timing_period = 1;          // episode launches: stamp timing events on every k-th one
   long long n_launch = 0;         // episode launches since the last reset
   // device buffers
@@ -370,6 +373,8 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   if (c->comm && rccl()) rccl()->commDestroy(c->comm);
   c->comm = nullptr;
   for (auto& ev : c->ring)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : c->cring)
     if (ev) (void)hipEventDestroy(ev);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -880,6 +885,7 @@ int p2pmg_reset_kernel_times(p2pmg_ctx* c) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->n_timed = 0;
   c->n_launch = 0;
+  c->n_coll = 0;
   return P2PMG_OK;
 }
 
@@ -1145,6 +1151,38 @@ int p2pmg_comm_init(p2pmg_ctx* c, const uint8_t id[128], int rank, int nranks) {
   return P2PMG_OK;
 }
 
+// HIP events around each data-path all-reduce (shared-table delta, DQN gradient), on the context's
+// stream, so the bench line can report what the exchange step costs at world > 1
+static hipError_t coll_mark(p2pmg_ctx* c, int end) {
+  if (c->cring.empty()) {
+    c->cring.assign(2 * p2pmg_ctx::kCRing, nullptr);
+    for (auto& ev : c->cring) {
+      const hipError_t e = hipEventCreate(&ev);
+      if (e != hipSuccess) return e;
+    }
+  }
+  const int slot = (int)(c->n_coll % p2pmg_ctx::kCRing);
+  const hipError_t e = hipEventRecord(c->cring[2 * slot + end], c->stream);
+  if (end) c->n_coll++;
+  return e;
+}
+
+int p2pmg_collective_ms(p2pmg_ctx* c, double* total_ms, int* count) {
+  if (!c || !total_ms || !count) return P2PMG_E_INVALID;
+  const long long n = c->n_coll < p2pmg_ctx::kCRing ? c->n_coll : p2pmg_ctx::kCRing;
+  double sum = 0.0;
+  for (long long k = c->n_coll - n; k < c->n_coll; ++k) {
+    const int slot = (int)(k % p2pmg_ctx::kCRing);
+    float ms = 0.0f;
+    HIP_TRY(c, hipEventSynchronize(c->cring[2 * slot + 1]));
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->cring[2 * slot], c->cring[2 * slot + 1]));
+    sum += ms;
+  }
+  *total_ms = sum;
+  *count = (int)n;
+  return P2PMG_OK;
+}
+
 int p2pmg_allreduce_q_delta(p2pmg_ctx* c) {
   if (!c) return P2PMG_E_INVALID;
   if (!c->qdelta) return fail(c, P2PMG_E_STATE, "allreduce_q_delta: context has no shared table");
@@ -1152,8 +1190,10 @@ int p2pmg_allreduce_q_delta(p2pmg_ctx* c) {
   Rccl* r = rccl();
   // ncclInt64 = 4, ncclSum = 0 (rccl.h)
   HIP_TRY(c, p2pmg::launch_fold_delta(c->qdelta, c->n_states * kQPad, c->stream));
+  HIP_TRY(c, coll_mark(c, 0));
   const int rc = r->allReduce(c->qdelta, c->qdelta, c->n_states * kQPad, 4, 0, c->comm, c->stream);
   if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclAllReduce: ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
+  HIP_TRY(c, coll_mark(c, 1));
   return P2PMG_OK;
 }
 
@@ -1518,8 +1558,10 @@ static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
     if (ranks) {
       Rccl* r = rccl();
       // ncclFloat32 = 7, ncclSum = 0: gradient sum over ranks (xGMI), 4609 floats
+      HIP_TRY(c, coll_mark(c, 0));
       const int rc = r->allReduce(c->d_gsum, c->d_gsum, p2pmg::kDqnParams, 7, 0, c->comm, c->stream);
       if (rc != 0) return fail(c, P2PMG_E_HIP, "dqn gradient all-reduce failed");
+      HIP_TRY(c, coll_mark(c, 1));
       HIP_TRY(c, p2pmg::launch_dqn_adam_shared(d, c->stream));
     }
   } else {

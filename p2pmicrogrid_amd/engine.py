@@ -302,6 +302,13 @@ class DeviceCommunityBatch:
         self._chk(self.L.p2pmg_kernel_times(self._ctx, out, max_n, C.byref(n)), "kernel_times")
         return out[:n.value].copy()
 
+    def collective_ms(self):
+        """(total ms, count) of the data-path RCCL all-reduces (shared-table delta, DQN gradient)
+        since the last reset_kernel_times (HIP events on the context's stream; syncs)."""
+        ms, n = C.c_double(0.0), C.c_int(0)
+        self._chk(self.L.p2pmg_collective_ms(self._ctx, C.byref(ms), C.byref(n)), "collective_ms")
+        return float(ms.value), int(n.value)
+
     def reset_kernel_times(self):
         self._chk(self.L.p2pmg_reset_kernel_times(self._ctx), "reset_kernel_times")
 
