@@ -777,11 +777,6 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       w2c[kk] = th0[kOffW2 + col * kH + 16 * g4 + kk];  // dH1's K order: unit 16 g4 + kk
     }
   }
-#ifdef P2PMG_TRAIN_SKEW  // timing experiment: the second half of the grid starts later
-  if (blockIdx.x >= gridDim.x / 2) {
-    for (int k = 0; k < P2PMG_TRAIN_SKEW; ++k) __builtin_amdgcn_s_sleep(127);
-  }
-#endif
   // the first agent's batch (explicit batch, or the sample pre-pass output)
   if (d.batch) {
     for (int k = threadIdx.x; k < kB * kTrans; k += 256) smpb[0][k] = d.batch[k];
@@ -821,6 +816,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     // ---- layer 1 (K = 5 padded to 8): Z1 = X W1 + b1, 6 target + 2 online row tiles
     const float bt0 = W.bt0, bo0 = W.bo0, bt1 = W.bt1, bo1 = W.bo1, b1t = W.b1t, b1o = W.b1o;
     unsigned z1mask = 0;  // online rows where z1 > 0 (ReLU derivative), bit 4 rt + r
+    __builtin_amdgcn_s_setprio(2);  // MFMA phase (see layer 2)
     // all 16 products first (8 independent accumulators), then the bias / ReLU / LDS stores: no
     // store waits on the MFMA it follows
     f32x4 z1[8];
@@ -854,13 +850,15 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       }
       *reinterpret_cast<float4*>(&H1oT[col][16 * rt + 4 * g4]) = make_float4(h[0], h[1], h[2], h[3]);
     }
+    __builtin_amdgcn_s_setprio(0);
     DQN_STAMP(0);
     __syncthreads();
     DQN_STAMP(1);
 
-#ifdef P2PMG_TRAIN_PRIO
+    // The MFMA phases (layers 1 and 2, the backward products) run at raised wave priority: the
+    // SIMD's other wave (another workgroup, in a VALU / LDS phase) then issues into the MFMA shadow
+    // instead of competing with the MFMA stream (configs[4] 14.55 -> 13.93 ms per episode)
     __builtin_amdgcn_s_setprio(2);
-#endif
     // ---- layer 2 as Z2^T = W2^T H1^T (K = 64): the operands of H1 W2 with the MFMA's A and B
     // swapped, so the accumulator of row tile rt holds data row 16 rt + c16 at the hidden units
     // h0 + r.  Layer 3 then sums 4 units in-lane and the 4 row groups with two exchanges, instead
@@ -879,9 +877,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       ao[0] = mfma4(bo, H1oT[k][c16], ao[0]);
       ao[1] = mfma4(bo, H1oT[k][16 + c16], ao[1]);
     }
-#ifdef P2PMG_TRAIN_PRIO
     __builtin_amdgcn_s_setprio(0);
-#endif
     DQN_STAMP(2);
     // ---- layer 3, this wave's 16 units: in-lane over r (a pairwise tree), then over the 4 row
     // groups for four tiles at once (reduce4_groups: 3 lane swaps + 3 adds, row group g4 ends with
@@ -965,9 +961,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     DQN_STAMP(4);
     __syncthreads();
     DQN_STAMP(1);
-#ifdef P2PMG_TRAIN_PRIO
     __builtin_amdgcn_s_setprio(2);
-#endif
     // Every operand of the backward products is read from LDS up front (16-B reads where the K
     // order allows), so the MFMA chains below never wait on a read between two products.
     // dW2 = H1^T dZ2 over the 32 data rows in the K order b = 8 g4 + q: A = H1oT[16 mt + c16][b]
@@ -1022,9 +1016,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
         gb1 += dz1;
         gW1[rt] = mfma4(xa[rt][r], dz1, gW1[rt]);
       }
-#ifdef P2PMG_TRAIN_PRIO
     __builtin_amdgcn_s_setprio(0);
-#endif
     if (has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
     DQN_STAMP(5);
     __syncthreads();  // every wave is done with this agent's LDS and with the online W2
