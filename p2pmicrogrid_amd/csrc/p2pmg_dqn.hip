@@ -699,13 +699,14 @@ __device__ __forceinline__ void batch_put(float* dst, int t, float v0, float v1)
 // layers 2 and 3: the 4 hidden units 16 w + 4 g4 + r of the transposed tiles).  Per-agent networks
 // read W2 per MFMA step from L1/L2; a shared network keeps its 48 W2 operands in registers.
 struct TrainW {
-  float bt0, bo0, bt1, bo1, b1t, b1o, b3t, b3o;
+  float bt0, bo0, bo1, b1t, b1o, b3t, b3o, w14t, w14o;  // layer 1: W1[g4][col], W1[4][col] (g4 = 0), biases
   float b2t[4], w3t[4], b2o[4], w3o[4];  // layer 2/3 of the hidden units 16 w + 4 g4 + r
 };
 __device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const float* tg, int col, int g4, int h0) {
   W.bt0 = tg[kOffW1 + g4 * kH + col];
   W.bo0 = th[kOffW1 + g4 * kH + col];
-  W.bt1 = g4 == 0 ? tg[kOffW1 + 4 * kH + col] : 0.0f;
+  W.w14t = tg[kOffW1 + 4 * kH + col];
+  W.w14o = th[kOffW1 + 4 * kH + col];
   W.bo1 = g4 == 0 ? th[kOffW1 + 4 * kH + col] : 0.0f;
   W.b1t = tg[kOffB1 + col];
   W.b1o = th[kOffB1 + col];
@@ -751,13 +752,13 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
   const int c16 = l & 15, g4 = l >> 4;
   const int col = 16 * w + c16;     // this lane's column of layer 1 and of dH1
   const int h0 = 16 * w + 4 * g4;   // this lane's 4 hidden units of layer 2 (transposed tiles)
-  const int xc = c16 < 5 ? c16 : 4;  // dW1: this lane's input feature
   const size_t A = (size_t)p.A;
 
   f32x4 gW2[4], gW1[2];
 #pragma unroll
   for (int m = 0; m < 4; ++m) gW2[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   gW1[0] = gW1[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float gx1[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   float gb1 = 0.0f, gb3 = 0.0f;
   float gb2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gW3[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   const int n_ag = d.batch ? 1 : d.apb;
@@ -813,12 +814,13 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     batch_part_at(d, min(a + 1, a_last), threadIdx.x, (int)min((unsigned)slot_n, (unsigned)(d.cap - 1)), nx0, nx1);
     slot_n = batch_slot(d, min(a + 2, a_last), threadIdx.x);
 
-    // ---- layer 1 (K = 5 padded to 8): Z1 = X W1 + b1, 6 target + 2 online row tiles
-    const float bt0 = W.bt0, bo0 = W.bo0, bt1 = W.bt1, bo1 = W.bo1, b1t = W.b1t, b1o = W.b1o;
+    // ---- layer 1: Z1 = X W1 + b1, 6 target + 2 online row tiles (K = 4 on MFMA, the action term
+    // K = 4 as an fmaf for target tiles, a second MFMA for online tiles)
+    const float bt0 = W.bt0, bo0 = W.bo0, bo1 = W.bo1, b1t = W.b1t, b1o = W.b1o;
     unsigned z1mask = 0;  // online rows where z1 > 0 (ReLU derivative), bit 4 rt + r
     __builtin_amdgcn_s_setprio(2);  // MFMA phase (see layer 2)
-    // all 16 products first (8 independent accumulators), then the bias / ReLU / LDS stores: no
-    // store waits on the MFMA it follows
+    // all products first (8 independent accumulators), then the bias / ReLU / LDS stores: no store
+    // waits on the MFMA it follows
     f32x4 z1[8];
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt) {
@@ -827,24 +829,27 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     }
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) z1[6 + rt] = mfma4(smp[16 * rt + c16][g4], bo0, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
-#pragma unroll
-    for (int rt = 0; rt < 6; ++rt) {
-      const int row = 16 * rt + c16, act = row / kB;
-      const float av = act == 0 ? 0.0f : (act == 1 ? 0.5f : 1.0f);
-      z1[rt] = mfma4(g4 == 0 ? av : 0.0f, bt1, z1[rt]);
-    }
+#ifndef P2PMG_L1O
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) z1[6 + rt] = mfma4(g4 == 0 ? smp[16 * rt + c16][4] : 0.0f, bo1, z1[6 + rt]);
+#endif
+    // a target tile holds one action value (rows 16 rt .. + 15: action rt / 2), so its K = 4 term
+    // is a per-column fmaf, the same single rounding as an MFMA's second product would give
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) H1t[16 * rt + 4 * g4 + r][col] = relu(z1[rt][r] + b1t);
+      for (int r = 0; r < 4; ++r)
+        H1t[16 * rt + 4 * g4 + r][col] = relu(fmaf((rt >> 1) == 0 ? 0.0f : ((rt >> 1) == 1 ? 0.5f : 1.0f), W.w14t, z1[rt][r]) + b1t);
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
       float h[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+#ifdef P2PMG_L1O
+        const float z = fmaf(smp[16 * rt + 4 * g4 + r][4], W.w14o, z1[6 + rt][r]) + b1o;
+#else
         const float z = z1[6 + rt][r] + b1o;
+#endif
         h[r] = relu(z);
         if (z > 0.0f) z1mask |= 1u << (4 * rt + r);
       }
@@ -989,14 +994,6 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       }
     // dW1's A operand: input feature c16 (< 5) of data rows b = 16 rt + 4 g4 + r (lanes c16 >= 5 read
     // feature 4 and select 0: no exec-masked read)
-    float xa[2][4];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float x = smp[16 * rt + 4 * g4 + r][xc];
-        xa[rt][r] = c16 < 5 ? x : 0.0f;
-      }
 #pragma unroll
     for (int q = 0; q < 8; ++q)
 #pragma unroll
@@ -1014,7 +1011,11 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       for (int rt = 0; rt < 2; ++rt) {
         const float dz1 = ((z1mask >> (4 * rt + r)) & 1u) ? acc[rt][r] : 0.0f;
         gb1 += dz1;
-        gW1[rt] = mfma4(xa[rt][r], dz1, gW1[rt]);
+        // dW1 = X^T dZ1 on VALU: this lane's partial over its 8 data rows, reduced over the row
+        // groups once per launch (5 useful output rows of 16 made the MFMA form mostly padding)
+        const float* xr = smp[16 * rt + 4 * g4 + r];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) gx1[k] = fmaf(xr[k], dz1, gx1[k]);
       }
     __builtin_amdgcn_s_setprio(0);
     if (has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
@@ -1031,6 +1032,11 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
 #endif
 
   gb1 = sum_groups(gb1);
+  float g1t[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) g1t[k] = sum_groups(gx1[k]);
+  // lane (g4, r) owns dW1 row 4 g4 + r (< 5): g4 = 0 rows 0..3, g4 = 1 row 4
+  auto dw1 = [&](int r) { return g4 == 0 ? g1t[r] : g1t[4]; };
 #pragma unroll
   for (int r = 0; r < 4; ++r) {  // over the 16 data-row lanes of each row group
     gb2[r] = sum16(gb2[r]);
@@ -1052,7 +1058,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int k = 4 * g4 + r;
-      if (k < 5) adam_update(d, th, tg, mm, vv, kOffW1 + k * kH + col, fminf(fmaxf(gW1[0][r] + gW1[1][r], -d.clip), d.clip), lr);
+      if (k < 5) adam_update(d, th, tg, mm, vv, kOffW1 + k * kH + col, fminf(fmaxf(dw1(r), -d.clip), d.clip), lr);
     }
     if (g4 == 0) adam_update(d, th, tg, mm, vv, kOffB1 + col, gb1, lr);
     if (c16 == 0) {
@@ -1071,7 +1077,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       for (int r = 0; r < 4; ++r) gp[kOffW2 + (16 * mt + 4 * g4 + r) * kH + col] = gW2[mt][r];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (4 * g4 + r < 5) gp[kOffW1 + (4 * g4 + r) * kH + col] = gW1[0][r] + gW1[1][r];
+      if (4 * g4 + r < 5) gp[kOffW1 + (4 * g4 + r) * kH + col] = dw1(r);
     if (g4 == 0) gp[kOffB1 + col] = gb1;
     if (c16 == 0) {
 #pragma unroll
