@@ -699,14 +699,13 @@ __device__ __forceinline__ void batch_put(float* dst, int t, float v0, float v1)
 // layers 2 and 3: the 4 hidden units 16 w + 4 g4 + r of the transposed tiles).  Per-agent networks
 // read W2 per MFMA step from L1/L2; a shared network keeps its 48 W2 operands in registers.
 struct TrainW {
-  float bt0, bo0, bo1, b1t, b1o, b3t, b3o, w14t, w14o;  // layer 1: W1[g4][col], W1[4][col] (g4 = 0), biases
+  float bt0, bo0, bo1, b1t, b1o, b3t, b3o, w14t;  // layer 1: W1[g4][col], W1[4][col] (g4 = 0), biases
   float b2t[4], w3t[4], b2o[4], w3o[4];  // layer 2/3 of the hidden units 16 w + 4 g4 + r
 };
 __device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const float* tg, int col, int g4, int h0) {
   W.bt0 = tg[kOffW1 + g4 * kH + col];
   W.bo0 = th[kOffW1 + g4 * kH + col];
   W.w14t = tg[kOffW1 + 4 * kH + col];
-  W.w14o = th[kOffW1 + 4 * kH + col];
   W.bo1 = g4 == 0 ? th[kOffW1 + 4 * kH + col] : 0.0f;
   W.b1t = tg[kOffB1 + col];
   W.b1o = th[kOffB1 + col];
@@ -740,8 +739,12 @@ __device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const f
   do {               \
   } while (0)
 #endif
+// train workgroups per CU (waves per SIMD): 2 in the default build (about 220 VGPRs)
+#ifndef P2PMG_TRAIN_OCC
+#define P2PMG_TRAIN_OCC 2
+#endif
 template <bool SHARED>
-__global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) {  // 2 waves / SIMD
+__global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const DqnParams d) {
   __shared__ float smpb[2][kB * kTrans];  // this agent's batch and the next one's (prefetched)
   __shared__ float H1t[3 * kB][kLdsRow];
   __shared__ __attribute__((aligned(16))) float H1oT[kH][kLdsRowT];  // online layer-1 activations, unit-major
@@ -829,10 +832,8 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     }
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) z1[6 + rt] = mfma4(smp[16 * rt + c16][g4], bo0, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
-#ifndef P2PMG_L1O
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) z1[6 + rt] = mfma4(g4 == 0 ? smp[16 * rt + c16][4] : 0.0f, bo1, z1[6 + rt]);
-#endif
     // a target tile holds one action value (rows 16 rt .. + 15: action rt / 2), so its K = 4 term
     // is a per-column fmaf, the same single rounding as an MFMA's second product would give
 #pragma unroll
@@ -845,11 +846,7 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       float h[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-#ifdef P2PMG_L1O
-        const float z = fmaf(smp[16 * rt + 4 * g4 + r][4], W.w14o, z1[6 + rt][r]) + b1o;
-#else
         const float z = z1[6 + rt][r] + b1o;
-#endif
         h[r] = relu(z);
         if (z > 0.0f) z1mask |= 1u << (4 * rt + r);
       }
@@ -984,6 +981,13 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
     for (int q = 0; q < 8; ++q) db[q] = dZ2[8 * g4 + q][col];
     // dH1 = dZ2 W2^T (own columns n = col) in the K order unit 16 g4 + kk: A = dZ2[16 rt + c16][16 g4
     // .. + 15] (four 16-B reads per rt), B = W2[col][16 g4 + kk] (registers for a shared network)
+#if P2PMG_TRAIN_OCC >= 3  // register budget: dW2's products issue before dH1's operands are read
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) gW2[mt] = mfma4(ha[mt][q], db[q], gW2[mt]);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     float za[2][16];
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
@@ -994,10 +998,12 @@ __global__ __launch_bounds__(256, 2) void dqn_train_kernel(const DqnParams d) { 
       }
     // dW1's A operand: input feature c16 (< 5) of data rows b = 16 rt + 4 g4 + r (lanes c16 >= 5 read
     // feature 4 and select 0: no exec-masked read)
+#if P2PMG_TRAIN_OCC < 3
 #pragma unroll
     for (int q = 0; q < 8; ++q)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) gW2[mt] = mfma4(ha[mt][q], db[q], gW2[mt]);
+#endif
     f32x4 acc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
@@ -1102,6 +1108,14 @@ __global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kerne
   const int k = blockIdx.x * kRedParams + j;
   const int per = (n_partials + kRedSlices - 1) / kRedSlices;
   const int b0 = sl * per, b1 = min(n_partials, b0 + per);
+  // the Adam state of this parameter, loaded ahead of the partials (one memory round trip less)
+  float m0 = 0.0f, v0 = 0.0f, w0 = 0.0f, tg0 = 0.0f;
+  if (sl == 0 && adam && k < kDqnParams) {
+    m0 = d.adam_m[k];
+    v0 = d.adam_v[k];
+    w0 = d.theta[k];
+    tg0 = d.target[k];
+  }
   float s = 0.0f;
   if (k < kDqnParams) {
     const float* g = d.grad + k;
@@ -1127,7 +1141,14 @@ __global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kerne
   }
   float gk = t * d.inv_agents;
   if (k < kOffB1) gk = fminf(fmaxf(gk, -d.clip), d.clip);
-  adam_update(d, d.theta, d.target, d.adam_m, d.adam_v, k, gk, d.lr_t);
+  // adam_update's arithmetic on the preloaded state
+  m0 = m0 + (gk - m0) * d.b1c;
+  v0 = v0 + (gk * gk - v0) * d.b2c;
+  w0 = w0 - (m0 * d.lr_t) / (sqrtf(v0) + d.adam_eps);
+  d.adam_m[k] = m0;
+  d.adam_v[k] = v0;
+  d.theta[k] = w0;
+  d.target[k] = d.tau_c * tg0 + d.tau * w0;
 }
 
 // shared network: mean over every agent (all ranks after the all-reduce), clip, Adam, soft update
@@ -1195,6 +1216,8 @@ hipError_t launch_dqn_act(const DqnParams& d, hipStream_t st) {
   }
   return hipGetLastError();
 }
+
+int dqn_train_blocks_per_cu() { return P2PMG_TRAIN_OCC; }
 
 hipError_t launch_dqn_train(const DqnParams& d, int blocks, bool shared_partials, hipStream_t st) {
   if (shared_partials)

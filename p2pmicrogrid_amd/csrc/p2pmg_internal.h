@@ -102,6 +102,7 @@ struct DqnParams {
 hipError_t launch_dqn_act(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_sample(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_train(const DqnParams& p, int blocks, bool shared_partials, hipStream_t stream);
+int dqn_train_blocks_per_cu();  // train workgroups resident per CU (the build's occupancy target)
 // sum of the train workgroups' partials (+ adam: the Adam step on it; else the sum goes to gsum)
 hipError_t launch_dqn_reduce_adam(const DqnParams& p, int n_partials, bool adam, hipStream_t stream);
 hipError_t launch_dqn_adam_shared(const DqnParams& p, hipStream_t stream);

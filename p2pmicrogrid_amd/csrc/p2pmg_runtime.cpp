@@ -1349,7 +1349,9 @@ int p2pmg_dqn_setup(p2pmg_ctx* c, const p2pmg_dqn_config* cfg) {
   HIP_TRY(c, dmalloc(&c->d_v, nn));
   for (float* b : {c->d_theta, c->d_target, c->d_m, c->d_v}) HIP_TRY(c, hipMemsetAsync(b, 0, nn * 4, c->stream));
   if (c->cfg.shared_q) {
-    int apb = cfg->agents_per_block > 0 ? cfg->agents_per_block : (int)((A + 511) / 512);  // 512 workgroups = 2 per CU
+    // default: one wave of train workgroups (2 per CU in the default build: 512 on 256 CUs)
+    const size_t slots = (size_t)c->n_cu * (size_t)p2pmg::dqn_train_blocks_per_cu();
+    int apb = cfg->agents_per_block > 0 ? cfg->agents_per_block : (int)((A + slots - 1) / slots);
     c->d_apb = apb < 1 ? 1 : apb;
     c->d_blocks = (int)((A + c->d_apb - 1) / c->d_apb);
     HIP_TRY(c, dmalloc(&c->d_grad, (size_t)c->d_blocks * NS));

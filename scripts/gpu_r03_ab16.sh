@@ -7,4 +7,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_dqn.py tests/test_gpu_dqn_a
 tail -1 "$O/pytest.log"
 P2PMG_LIB="$R/build/ab/l1o.so" timeout -k 10 600 python -u -m pytest tests/test_gpu_dqn.py tests/test_gpu_dqn_api.py -m gpu -x -q --timeout 300 --timeout-method thread > "$O/pytest_l1o.log" 2>&1 || { tail -40 "$O/pytest_l1o.log"; exit 1; }
 tail -1 "$O/pytest_l1o.log"
-bash scripts/gpu_ab.sh config5 2 build/ab/cur.so build/ab/cur2.so build/ab/l1o.so
+bash scripts/gpu_ab.sh config5 2 build/ab/cur.so build/ab/cur2.so build/ab/l1o.so build/ab/redp.so
