@@ -128,7 +128,11 @@ def test_full_size_config5_dqn_per_agent_sampled_oracle():
     eng.close()
 
 
-def test_full_size_config5_dqn_shared_network_properties():
+def test_full_size_config5_dqn_shared_network_properties(monkeypatch):
+    """The benched configs[4] shape: engine a acts with the MFMA act kernel (16 agents per
+    workgroup), engine b with the one-wave-per-agent kernel (P2PMG_DQN_ACT=wave, checked against the
+    oracle at small S): every record, the replay draws behind the trained weights and the weights
+    themselves agree bit for bit over all 8,192 agents (and the deterministic gradient reduction)."""
     from p2pmicrogrid_amd.dataset import scenario_batch
     S, N, R, T = 4096, 2, 1, 96
     inp = scenario_batch(S, N, T)
@@ -137,11 +141,15 @@ def test_full_size_config5_dqn_shared_network_properties():
     w0 = a.get_weights("online")
     for e, (mode, eps) in enumerate((("fill", 1.0), ("train", 0.9), ("train", 0.81))):
         for x in (a, b):
+            if x is b:
+                monkeypatch.setenv("P2PMG_DQN_ACT", "wave")
             x.run_episode(mode, "philox", episode=e, epsilon=eps, record=("reward", "p2p", "action"))
+            monkeypatch.delenv("P2PMG_DQN_ACT", raising=False)
             x.reset_temperatures_philox(e + 1, 0.3)
+        assert a.last_kernel() == "dqn_act_shared_kernel<2>" and b.last_kernel() == "dqn_act_kernel<2>"
         ra, rb = a.get_records(("reward", "p2p", "action")), b.get_records(("reward", "p2p", "action"))
         for k in ra:
-            assert np.array_equal(ra[k], rb[k]), (e, k)  # deterministic reduction: same bits
+            assert np.array_equal(ra[k], rb[k]), (e, k)  # same Q values, draws and reduction: same bits
         assert np.all(np.isfinite(ra["reward"])) and np.all(ra["action"] <= 2)
         assert np.all(ra["p2p"].sum(axis=-1) == 0)  # N = 2: the P2P exchange is antisymmetric
     wa, wb = a.get_weights("online"), b.get_weights("online")
