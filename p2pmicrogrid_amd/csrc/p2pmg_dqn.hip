@@ -407,6 +407,25 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
     w3[r] = th[kOffW3 + 16 * w + 4 * g4 + r];
   }
   const float b3 = th[kOffB3];
+  // every round's exploration draw (or replayed code) ahead of the rounds: they depend only on
+  // (t, episode, agent), so they run under the prologue's load latency, off the rounds' chain
+  uint64_t codes_pack = ~0ull;  // byte r: code of round r (255 = greedy), up to 8 rounds
+  if (agent_thr && !greedy_mode && R1 <= 8) {
+    if (p.rng == 0) {
+      for (int w4 = 0; w4 < W; ++w4)
+        codes_pack = (codes_pack & ~(0xFFFFFFFFull << (32 * w4))) |
+                     ((uint64_t)p.codes[((size_t)t * W + w4) * A + a] << (32 * w4));
+    } else {
+      for (int q = 0; 2 * q < R1; ++q) {  // one Philox block per two rounds (oracle/philox.py::decision_draws)
+        uint32_t c0 = (uint32_t)(t * ((R1 + 1) >> 1) + q), c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
+                 c3 = kTagDecision;
+        philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
+        const uint64_t k0 = (double)c0 * (1.0 / 4294967296.0) < p.eps ? __umulhi(c1, 3u) : 255u;
+        const uint64_t k1 = (double)c2 * (1.0 / 4294967296.0) < p.eps ? __umulhi(c3, 3u) : 255u;
+        codes_pack = (codes_pack & ~(0xFFFFull << (16 * q))) | (k0 << (16 * q)) | (k1 << (16 * q + 8));
+      }
+    }
+  }
   const int tag4 = reduce4_tag();
 
   if (tid < AG * N) shP[0][tid] = 0.0f;
@@ -429,7 +448,9 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
       p2pf = div_n<N>(acc) / mi;
       code = 255;  // ActorModel.select_action rl.py:174-183: explore draw, else greedy
       if (!greedy_mode) {
-        if (p.rng == 0) {
+        if (R1 <= 8) {
+          code = (int)((codes_pack >> (8 * r)) & 0xFFu);
+        } else if (p.rng == 0) {
           code = (int)((p.codes[((size_t)t * W + (r >> 2)) * A + a] >> (8 * (r & 3))) & 0xFFu);
         } else {
           uint32_t c0 = (uint32_t)(t * ((R1 + 1) >> 1) + (r >> 1)), c1 = (uint32_t)p.episode,

@@ -273,7 +273,8 @@ def test_shared_act_mfma_kernel_equals_wave_kernel(S, N, R, monkeypatch):
     """A shared network's act launch on MFMA tiles (dqn_act_shared_kernel, 16 agents per workgroup,
     partial last workgroup when 16 / N does not divide S) gives bitwise the records, replay rings,
     sampled slots and trained weights of the one-wave-per-agent kernel (P2PMG_DQN_ACT=wave): same
-    fmaf chain over k in layer 2, same pairwise tree over the 64 units in layer 3."""
+    fmaf chain over k in layer 2, same pairwise tree over the 64 units in layer 3; Philox and
+    replay-mode exploration and replay draws."""
     T = 24
     runs = []
     for kind in ("wave", "mfma"):
@@ -295,6 +296,14 @@ def test_shared_act_mfma_kernel_equals_wave_kernel(S, N, R, monkeypatch):
             recs.append(eng.get_records(list(keys) + (["loss"] if mode == "train" else [])))
             recs.append({"episode_reward": eng.episode_reward()})
             eng.reset_temperatures_philox(ep + 1)
+        # a replay-mode training episode: uploaded codes (prefetched as words) and deque samples
+        rs = np.random.RandomState(S * 100 + N)
+        codes = rs.choice(np.array([0, 1, 2, 255, 255, 255], np.uint8), size=(T, R + 1, S * N))
+        samples = np.stack([np.stack([rs.choice(96, 32, replace=False) for _ in range(S * N)]) for _ in range(T)])
+        eng.set_replay_codes(codes)
+        eng.set_samples(samples)
+        eng.run_episode("train", "replay", episode=9, epsilon=0.5, record=keys + ("loss",))
+        recs.append(eng.get_records(list(keys) + ["loss"]))
         eng.run_episode("greedy", record=keys)
         recs.append(eng.get_records(list(keys)))
         buf, added = eng.get_buffer()
