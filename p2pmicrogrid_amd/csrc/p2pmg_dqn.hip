@@ -301,19 +301,19 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
 }
 
 // ----------------------------------------------------------------- act, one shared network
-// dqn_act_shared_kernel<N>: the same env step as dqn_act_kernel for ONE network shared by every
-// agent (configs[4]), with the greedy forwards of 16 agents on MFMA tiles.  A 256-thread workgroup
-// owns kActAgents / N scenarios (16 agents).  Per round, thread j < 16 does agent j's scalar work
-// (observation, exploration draw, divide-power row); the 48 greedy rows (3 actions x 16 agents) go
-// through layer 1 on VALU (thread = hidden unit x 4 agents), layer 2 as Z2^T = W2^T H1^T on
+// dqn_act_shared_kernel<N, AGW>: the same env step as dqn_act_kernel for ONE network shared by
+// every agent (configs[4]), with the greedy forwards of AGW agents on MFMA tiles.  A 256-thread
+// workgroup owns AGW / N scenarios.  Per round, thread j < AGW does agent j's scalar work
+// (observation, divide-power row); the 3 AGW greedy rows (3 actions x AGW agents) go
+// through layer 1 on VALU (thread = hidden unit x AGW / 4 agents), layer 2 as Z2^T = W2^T H1^T on
 // v_mfma_f32_16x16x4_f32 (wave w owns hidden units 16w..16w+15; its 16 W2 operands stay in
 // registers for the launch; the shared W2 is read once per workgroup instead of once per agent and
 // round), layer 3 in-lane.  Bitwise the same Q values as dqn_act_kernel: the f32 MFMA accumulates
 // its K products as an fmaf chain in k order (the VALU loop's order), and layer 3's sum over the 64
 // units is the same pairwise tree (4 units in-lane, the 16-lane row groups over lane ^ 16 and
 // lane ^ 32, then the 4 waves pairwise) as wave_sum over lane = unit.
-constexpr int kActAgents = 16;
-constexpr int kActRows = 3 * kActAgents;  // row = action * 16 + agent slot
+// AGW agent slots per workgroup (16, or 8 for more, shorter workgroups); row = action * AGW + slot,
+// in MT = ceil(3 AGW / 16) row tiles
 
 #ifndef P2PMG_TRACE
 #define P2PMG_TRACE 0
@@ -331,24 +331,27 @@ constexpr int kActRows = 3 * kActAgents;  // row = action * 16 + agent slot
   do {               \
   } while (0)
 #endif
-template <int N>
+template <int N, int AGW>
 __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) {
-  constexpr int SPW = kActAgents / N;  // scenarios per workgroup
-  constexpr int AG = SPW * N;          // agents per workgroup (<= 16)
+  static_assert(AGW == 8 || AGW == 16, "8 or 16 agent slots per workgroup");
+  constexpr int SPW = AGW / N;          // scenarios per workgroup
+  constexpr int AG = SPW * N;           // agents per workgroup (<= AGW)
+  constexpr int MT = (3 * AGW + 15) / 16;  // row tiles of the greedy forward
+  constexpr int SPT = AGW / 4;          // layer-1 agent slots per thread (4 waves)
   const EpisodeParams& p = d.e;
 #if P2PMG_TRACE
   uint64_t atr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, alast;
   asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(alast)::"memory");
 #endif
   __shared__ float shP[2][AG * N];
-  __shared__ float4 shX[kActAgents];   // time, normalised T_in, balance, p2p of agent slot j
-  __shared__ float H1[kActRows][kLdsRow];
-  __shared__ float qpart[4][kActRows + 16];  // + the 4th (unused) tile of reduce4_groups
+  __shared__ float4 shX[AGW];   // time, normalised T_in, balance, p2p of agent slot j
+  __shared__ float H1[16 * MT][kLdsRow];
+  __shared__ float qpart[4][64];  // 4 tiles of reduce4_groups (MT used)
   __shared__ float shR[AG];
-  __shared__ int shN[kActAgents];
-  __shared__ float shEp[kActAgents];
+  __shared__ int shN[AGW];
+  __shared__ float shEp[AGW];
   __shared__ int shFlag[2];
-  __shared__ __attribute__((aligned(16))) int shI[kActAgents][kB];  // Floyd draws of the replay sample
+  __shared__ __attribute__((aligned(16))) int shI[AGW][kB];  // Floyd draws of the replay sample
   const int tid = threadIdx.x;
   const int w = tid / kWave, l = tid % kWave;
   const int c16 = l & 15, g4 = l >> 4;
@@ -465,30 +468,30 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
     }
     ACT_STAMP(1);
     if (__syncthreads_or(greedy)) {
-      // layer 1: the three action rows of agent slots 4 (tid / 64) .. + 3 at unit u
+      // layer 1: the three action rows of agent slots SPT w .. + SPT - 1 at unit u
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ag = 4 * w + q;
+      for (int q = 0; q < SPT; ++q) {
+        const int ag = SPT * w + q;
         const float4 x = shX[ag];
         float z = x.w * w13;
         z = fmaf(x.z, w12, z);
         z = fmaf(x.y, w11, z);
         z = fmaf(x.x, w10, z);
         H1[ag][u] = relu(z + b1);
-        H1[kActAgents + ag][u] = relu(fmaf(0.5f, w14, z) + b1);
-        H1[2 * kActAgents + ag][u] = relu((z + w14) + b1);
+        H1[AGW + ag][u] = relu(fmaf(0.5f, w14, z) + b1);
+        H1[2 * AGW + ag][u] = relu((z + w14) + b1);
       }
       __syncthreads();
-      f32x4 acc[3];
+      f32x4 acc[MT];
 #pragma unroll
-      for (int rt = 0; rt < 3; ++rt) acc[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      for (int rt = 0; rt < MT; ++rt) acc[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int kk = 0; kk < 16; ++kk)
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt) acc[rt] = mfma4(w2[kk], H1[16 * rt + c16][4 * kk + g4], acc[rt]);
-      float sq[3];
+        for (int rt = 0; rt < MT; ++rt) acc[rt] = mfma4(w2[kk], H1[16 * rt + c16][4 * kk + g4], acc[rt]);
+      float sq[3] = {0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int rt = 0; rt < 3; ++rt) {
+      for (int rt = 0; rt < MT; ++rt) {
         float v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = relu(acc[rt][q] + b2[q]) * w3[q];
@@ -504,7 +507,7 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
         float qv[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          const int row = 16 * k + j;
+          const int row = AGW * k + j;
           qv[k] = ((qpart[0][row] + qpart[1][row]) + (qpart[2][row] + qpart[3][row])) + b3;
         }
         act = 0;
@@ -584,7 +587,10 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
   // indices of the earlier ones, so after pass k the first k draws are final and a pass that changes
   // nothing has reached the sequential result (typically 2 passes instead of 32 serial steps).
   if (p.mode == 0 && d.fused_sample) {
-    const int aj = tid >> 4, q0 = tid & 15, q1 = q0 + 16;
+    // AGW = 16: 16 threads per agent, draws q0 and q0 + 16; AGW = 8: 32 threads per agent, one draw
+    // each (the second draw duplicates the first: same result, written twice)
+    constexpr int TPA = 256 / AGW;
+    const int aj = tid / TPA, q0 = tid % TPA, q1 = TPA == 16 ? q0 + 16 : q0;
     const bool va = aj < AG && s0 + aj / N < p.S;
     const int a2 = va ? s0 * N + aj : 0;
     const int n_add = va ? shN[aj] : kB;
@@ -598,6 +604,10 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
       int r[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
+        if (h == 1 && TPA != 16) {
+          r[1] = r[0];
+          break;
+        }
         const int q = h ? q1 : q0;
         uint32_t c0 = (uint32_t)t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a2, c3 = kTagSample + (uint32_t)q;
         philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
@@ -1210,12 +1220,15 @@ __global__ void dqn_forward_kernel(const float* __restrict__ th, int n, const fl
 }  // namespace
 
 hipError_t launch_dqn_act(const DqnParams& d, hipStream_t st) {
-  if (d.n_nets == 1 && !d.act_wave) {  // one shared network: 16 agents per workgroup on MFMA tiles
+  if (d.n_nets == 1 && !d.act_wave) {  // one shared network: AGW agents per workgroup on MFMA tiles
+#ifndef P2PMG_ACT_AGW
+#define P2PMG_ACT_AGW 16
+#endif
     switch (d.e.N) {
 #define P2PMG_DQN_ACT_SHARED(NN)                                                                               \
   case NN: {                                                                                                   \
-    constexpr int spw = kActAgents / NN;                                                                       \
-    hipLaunchKernelGGL(dqn_act_shared_kernel<NN>, dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d);         \
+    constexpr int agw = NN <= 8 ? P2PMG_ACT_AGW : 16, spw = agw / NN;                                          \
+    hipLaunchKernelGGL((dqn_act_shared_kernel<NN, agw>), dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d); \
     break;                                                                                                     \
   }
       P2PMG_DQN_ACT_SHARED(1) P2PMG_DQN_ACT_SHARED(2) P2PMG_DQN_ACT_SHARED(3) P2PMG_DQN_ACT_SHARED(4)
