@@ -145,8 +145,17 @@ def launch_ranks(argv, gpus: int) -> int:
             env["P2PMG_BENCH_DEVICE"] = str(r % n_dev)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    # wait for every rank; if one fails, stop the others (they would wait in a collective forever)
+    import time as _t
+    while any(p.poll() is None for p in procs):
+        if any(p.poll() not in (None, 0) for p in procs):
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        _t.sleep(0.2)
     out0, _ = procs[0].communicate()
-    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    rcs = [p.wait() for p in procs]
     line = None
     for ln in (out0 or "").splitlines():
         ln = ln.strip()

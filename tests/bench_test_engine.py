@@ -9,6 +9,10 @@ from p2pmicrogrid_amd.distributed import Shard
 
 class BenchOracleEngine(OracleEngine):
     def __init__(self, S, N, R, T, q_dtype="f64", device=0, scenario_offset=0, shared_q=False, seed=42):
+        import os
+        fail = os.environ.get("P2PMG_BENCH_TEST_FAIL_RANK")
+        if fail is not None and fail == os.environ.get("RANK"):
+            raise RuntimeError("test: this rank fails at engine construction")
         super().__init__(Shard(0, 1, scenario_offset, S), S, N, R, T, q_dtype, device, seed, shared_q=shared_q)
         self.device = device
         self._times = []

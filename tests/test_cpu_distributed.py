@@ -123,3 +123,24 @@ def test_bench_rejects_world_mismatch():
     p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and "WORLD_SIZE=2" in (p.stderr + p.stdout)
+
+
+def test_bench_launcher_stops_surviving_ranks_when_one_fails():
+    """A rank that dies (here rank 1, at engine construction) must not leave rank 0 waiting in a
+    collective forever: the launcher kills the survivors and exits non-zero with the exit codes."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["P2PMG_BENCH_TEST_ENGINE"] = "bench_test_engine:BenchOracleEngine"
+    env["P2PMG_BENCH_TEST_FAIL_RANK"] = "1"
+    env["PYTHONPATH"] = os.pathsep.join([root, os.path.join(root, "tests"), env.get("PYTHONPATH", "")])
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--scenarios", "3", "--horizon", "12", "--no-cpu-baseline"]
+    t0 = time.time()
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200)
+    assert p.returncode != 0
+    assert "rank exit codes" in p.stderr
+    assert not [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert time.time() - t0 < 150
