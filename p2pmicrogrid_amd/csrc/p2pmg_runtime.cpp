@@ -443,7 +443,7 @@ int p2pmg_set_profiles(p2pmg_ctx* c, const float* load_w, const float* pv_w) {
   }
   {  // the battery rule's range-test-free variant needs bounded, finite balances (p2pmg_kernels.hip)
     bool ok = true;
-    for (size_t k = 0; k < n; ++k) ok &= (std::fabs(load_w[k]) <= 0x1p100f) & (std::fabs(pv_w[k]) <= 0x1p100f);
+    for (size_t k = 0; k < n; ++k) ok = ok && std::fabs(load_w[k]) <= 0x1p100f && std::fabs(pv_w[k]) <= 0x1p100f;
     c->prof_bounded = ok;
   }
   e = hipMemcpyAsync(dl, load_w, n * 4, hipMemcpyHostToDevice, c->stream);
