@@ -1087,11 +1087,7 @@ struct FastRec {         // [T][A], 32 B
   uint32_t ips;          // byte r: p2p bin of round r
 };
 // BAT: 0 none, 1 battery with per-lane range tests, 2 battery in the launcher-verified domain
-// HL (half-row loads; N = 2, f64 tables, no battery): each scenario takes a lane quad; the two idle
-// lanes of the quad load bytes 16..31 of their agent's 32-B row slot in the same 16-B load that
-// gives the agent bytes 0..15, so a row is one load instruction and one 32-B sector per lane pair
-// instead of a 16-B and an 8-B load; one DPP move returns the third value at its first use.
-template <int N, typename QT, int R1, bool TRAIN, int BAT, bool NARROW, bool HL = false>
+template <int N, typename QT, int R1, bool TRAIN, int BAT, bool NARROW>
 __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams p, const uint2* __restrict__ pre,
                                                              FastRec* __restrict__ recs, int spw, int n_cons,
                                                              const PrepOut nxt) {
@@ -1103,10 +1099,8 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     for (size_t k2 = (size_t)(blockIdx.x - n_cons) * kWave + threadIdx.x; k2 < n; k2 += stride) prepass_one(p, nxt, k2);
     return;
   }
-  constexpr int GL = pow2ceil(N);    // lanes of a scenario's agents
-  constexpr int G = HL ? 4 : GL;      // lanes per scenario
+  constexpr int G = pow2ceil(N);
   static_assert(G <= 8 && R1 >= 1 && R1 <= 4, "fast path: G <= 8, R + 1 <= 4");
-  static_assert(!HL || (N == 2 && sizeof(QT) == 8 && BAT == 0), "half-row loads: N = 2, f64, no battery");
   // N = 2: round 1's Q row is one of three (by the partner's round-0 action) whose bins the
   // pre-pass wrote; all three are issued a step ahead, so round 1 waits for no gather
   // (not with a battery: the partner's round-0 power then depends on its state of charge)
@@ -1130,30 +1124,9 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const int a_first = (int)blockIdx.x * spw * N;
   constexpr uint32_t kRowShift = sizeof(QT) == 8 ? 5 : 4;  // padded row: 32 B (f64) / 16 B (f32)
   const char* const qwave = reinterpret_cast<const char*>(p.q) + ((size_t)a_first * n_states << kRowShift);
-  const bool helper = HL && i >= N;  // an idle lane of the quad: loads the upper half of agent i - N's rows
-  const bool own_active = helper && sl < spw && s < p.S;
-  const uint32_t qlane = active       ? (uint32_t)(a - a_first) * (n_states << kRowShift)
-                         : own_active ? (uint32_t)(s * N + (i - N) - a_first) * (n_states << kRowShift) + 16u
-                         : (helper ? 16u : 0u);
+  const uint32_t qlane = active ? (uint32_t)(a - a_first) * (n_states << kRowShift) : 0u;
   auto gat = [&](uint32_t row) __attribute__((always_inline)) {
-    if constexpr (HL) {
-      const uint32_t ro = (uint32_t)__float_as_int(shfl_xor_c<2>(__int_as_float((int)row)));  // the agent's row
-      const uint32_t r = helper ? ro : row;
-      const double2 v = *reinterpret_cast<const double2*>(qwave + (qlane + (r << kRowShift)));
-      return Row4<QT>{{(QT)v.x, (QT)v.y, (QT)0, (QT)0}};
-    } else {
-      return gather_row(reinterpret_cast<const QT*>(qwave + (qlane + (row << kRowShift))));
-    }
-  };
-  // HL: the agent's third value is its helper lane's first (no-op otherwise)
-  auto resolve = [&](Row4<QT> r) __attribute__((always_inline)) {
-    if constexpr (HL) {
-      const double x = (double)r.v[0];
-      const int lo = __float_as_int(shfl_xor_c<2>(__int_as_float(__double2loint(x))));
-      const int hi = __float_as_int(shfl_xor_c<2>(__int_as_float(__double2hiint(x))));
-      r.v[2] = (QT)__hiloint2double(hi, lo);
-    }
-    return r;
+    return gather_row(reinterpret_cast<const QT*>(qwave + (qlane + (row << kRowShift))));
   };
   const int np = k.np;
   const int nbv = k.nb;
@@ -1300,7 +1273,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     }
     trMid = tr1;  // no candidate rows (N != 2 or a battery): "round1" runs from the rows' arrival
 #endif
-    row0 = patched(resolve(row0), a0, pat);  // ... may have hit a prefetched row
+    row0 = patched(row0, a0, pat);  // ... may have hit a prefetched row
 
     // round 0 (P = 0: every filtered power is -0, tot = 0, even split)
     int code = (int)(cw & 0xFF);
@@ -1336,12 +1309,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       // load; configs[1] 79.8 -> 79.0 us, configs[3] 66.2 -> 65.3 ms at the bench's epsilon)
       {
         Row4<QT> r0{};
-        bool need0 = ((cw1 & 0xFF) == 255) || (TRAIN && R1 == 1);
-        if constexpr (HL) {  // a helper lane loads when its agent does
-          const int no = __float_as_int(shfl_xor_c<2>(__int_as_float((int)need0)));
-          need0 = helper ? no != 0 : need0;
-        }
-        if (need0) r0 = gat(a0n);
+        if (((cw1 & 0xFF) == 255) || (TRAIN && R1 == 1)) r0 = gat(a0n);
         row0n = r0;
       }
 #endif
@@ -1383,7 +1351,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
 #pragma unroll
     for (int r = 1; r < R1; ++r) {
       if (r == 1) {
-        gather_even<N, 1, GL>(ev0, col, i);
+        gather_even<N, 1, G>(ev0, col, i);
       } else {
         exchange<N>(row, col, i, sl, nullptr);
       }
@@ -1405,7 +1373,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         }
 #endif
         ip = (int)((ipc0 >> (8 * b)) & 0xFFu);
-        rowR = patched(sel_row(b, resolve(cand[0]), resolve(cand[1]), resolve(cand[2])), strip + (uint32_t)ip, pat);
+        rowR = patched(sel_row(b, cand[0], cand[1], cand[2]), strip + (uint32_t)ip, pat);
       } else {
         float acc = 0.0f;
 #pragma unroll
@@ -1415,7 +1383,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
 #if P2PMG_ABLATE == 7
         rowR = fake_row(q + (need ? strip + (uint32_t)ip : a0) * kQPad);
 #else
-        rowR = resolve(gat((need ? strip + (uint32_t)ip : a0)));
+        rowR = gat((need ? strip + (uint32_t)ip : a0));
 #endif
       }
       act = code == 255 ? argmax3(rowR) : code;
@@ -1517,7 +1485,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       // QAgent.train agent.py:293-298 -> QActor.train rl.py:119-129
       const uint32_t srow = strip + (uint32_t)ip;
       const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
-      const QT qnew = td_update(qsa, rw, max3(patched(resolve(rowN), aN, pprev)), k.alpha, k.gamma);
+      const QT qnew = td_update(qsa, rw, max3(patched(rowN, aN, pprev)), k.alpha, k.gamma);
       *(active ? q + srow * kQPad + act : q_dummy) = qnew;
 #if P2PMG_ABLATE == 9 || P2PMG_ABLATE == 10
       pat = Patch<QT>{0xFFFFFFFFu, 0, (QT)0};  // timing-only: the next step does not wait for this TD
@@ -1622,25 +1590,9 @@ __global__ void fast_rec_unpack_kernel(int T, int R1, int A, uint32_t tb, const 
 
 // hipExtLaunchKernel stamps the start / stop events from the dispatch itself: no marker packets
 // between back-to-back episodes
-// half-row loads for N = 2 f64 tables (episode_fast_kernel's HL): opt-in, P2PMG_FAST_HL=1
-inline bool fast_hl_enabled() {
-  static const bool on = [] { const char* v = getenv("P2PMG_FAST_HL"); return v && v[0] == '1'; }();
-  return on;
-}
 template <int N, typename QT, int R1, int BAT, bool NARROW>
 void launch_fast_nw(const EpisodeParams& p, const uint2* pre, FastRec* recs, int blocks, int spw, int prod,
                     const PrepOut& nxt, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
-  if constexpr (N == 2 && sizeof(QT) == 8 && BAT == 0) {
-    if (spw <= kWave / 4 && fast_hl_enabled()) {
-      if (p.mode == 0)
-        hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, true, BAT, NARROW, true>), dim3(blocks + prod), dim3(kWave),
-                              0, st, ev0, ev1, 0, p, pre, recs, spw, blocks, nxt);
-      else
-        hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, false, BAT, NARROW, true>), dim3(blocks + prod), dim3(kWave),
-                              0, st, ev0, ev1, 0, p, pre, recs, spw, blocks, nxt);
-      return;
-    }
-  }
   if (p.mode == 0)
     hipExtLaunchKernelGGL((episode_fast_kernel<N, QT, R1, true, BAT, NARROW>), dim3(blocks + prod), dim3(kWave), 0, st,
                           ev0, ev1, 0, p, pre, recs, spw, blocks, nxt);
