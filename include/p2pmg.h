@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define P2PMG_ABI_VERSION 5  /* 3: p2pmg_episode_args.next_epsilon; 4: P2PMG_FLAG_NEXT_EPSILON, p2pmg_prepass_stats, per-network Adam steps; 5: p2pmg_collective_ms */
+#define P2PMG_ABI_VERSION 6  /* 3: p2pmg_episode_args.next_epsilon; 4: P2PMG_FLAG_NEXT_EPSILON, p2pmg_prepass_stats, per-network Adam steps; 5: p2pmg_collective_ms; 6: DQN gradient segments, p2pmg_dqn_set_exchange, p2pmg_dqn_grad_layout */
 
 typedef struct p2pmg_ctx p2pmg_ctx;
 
@@ -201,10 +201,11 @@ int p2pmg_last_kernel_ms(p2pmg_ctx* ctx, float* ms);           /* HIP-event time
  * (ring of the last 4096 launches, on the context's stream); *count = entries written. */
 int p2pmg_kernel_times(p2pmg_ctx* ctx, float* ms, int max, int* count);
 int p2pmg_reset_kernel_times(p2pmg_ctx* ctx);
-/* Sum of the HIP-event durations (ms) of the data-path RCCL all-reduces (shared-table delta,
- * DQN gradient; not the episode metrics) enqueued since p2pmg_reset_kernel_times, over the last
- * 1024 of them; *count = all-reduces summed.  No reference counterpart (the reference is one
- * process); the multi-GPU bench line reports it. */
+/* Sum of the HIP-event durations (ms) of the data-path collectives (shared-table delta
+ * all-reduce, DQN gradient-segment all-gather; not the episode metrics) enqueued since
+ * p2pmg_reset_kernel_times; *count = collectives summed (all of them: older ring slots are folded
+ * into a running total before reuse).  No reference counterpart (the reference is one process);
+ * the multi-GPU bench line reports it. */
 int p2pmg_collective_ms(p2pmg_ctx* ctx, double* total_ms, int* count);
 /* Stamp the episode kernel's timing events on every period-th episode launch only (default 1 =
  * every launch; the counter restarts here and at p2pmg_reset_kernel_times, so the next launch is
@@ -290,8 +291,15 @@ typedef struct p2pmg_dqn_config {
   double clip;     /* 1.0: first kernel's gradient clipped to [-clip, clip] (rl.py:329) */
   int32_t batch;   /* 32 (agent.py:308); the only supported value */
   int32_t capacity; /* 5000 (agent.py:308) */
-  int32_t agents_per_block; /* shared network: agents whose gradients one workgroup sums (0 = auto) */
-  int32_t reserved;
+  int32_t agents_per_block; /* shared network: agents whose gradients one workgroup sums (0 = auto:
+                               ceil(A / (CUs x workgroups per CU)), i.e. device- and shard-dependent) */
+  int32_t grad_segments;    /* shared network: the context's agents split into this many contiguous
+                               gradient segments of whole scenarios (0 = 1).  The gradient of an env
+                               step is sum over segments (in global segment order) of the segment's
+                               sum over its agents_per_block blocks (16 slices, fixed order): with
+                               agents_per_block and the TOTAL segment count fixed, 1 rank x G segments
+                               == W ranks x G/W segments bit for bit (rl.py:307-333 averaged over
+                               agents, build-defined) */
 } p2pmg_dqn_config;
 
 int p2pmg_dqn_config_default(p2pmg_dqn_config* cfg);
@@ -314,6 +322,21 @@ int p2pmg_dqn_set_buffer(p2pmg_ctx* ctx, int first, int count, const float* host
 int p2pmg_dqn_forward(p2pmg_ctx* ctx, int net, int n, const float* x, float* q);
 /* Trainer._train + update_targets (rl.py:307-359) of one network on a given batch [32][10] */
 int p2pmg_dqn_train_batch(p2pmg_ctx* ctx, int net, const float* batch, float* loss);
+
+/* Shared network over several ranks (config 5): the gradient segments of every rank are gathered
+ * once per env step, then every rank sums all of them in global segment order and takes the same
+ * Adam step, so the replicas stay bit-identical.  With an RCCL communicator (p2pmg_comm_init) the
+ * gather is an in-place ncclAllGather on the context's stream (xGMI).  Without one, a host exchange
+ * function does it: `segments` is [nranks][floats_per_rank] f32 host memory with this rank's part
+ * filled in; the function fills every other rank's part (an all-gather over any transport, e.g.
+ * gloo) and returns 0 (non-zero aborts the episode with P2PMG_E_STATE).  It is called
+ * synchronously from p2pmg_run_episode, on the calling thread, once per training env step.
+ * fn = NULL removes it (rank 0 of 1).  No reference counterpart (one process, rl.py:307-333). */
+typedef int (*p2pmg_exchange_fn)(void* user, float* segments, int64_t floats_per_rank, int rank, int nranks);
+int p2pmg_dqn_set_exchange(p2pmg_ctx* ctx, p2pmg_exchange_fn fn, void* user, int rank, int nranks);
+/* the shared-network gradient layout in use: segments of this context, agents per train
+ * workgroup, train workgroups per env step */
+int p2pmg_dqn_grad_layout(p2pmg_ctx* ctx, int* segments, int* agents_per_block, int* blocks);
 
 #ifdef __cplusplus
 }

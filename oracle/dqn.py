@@ -34,7 +34,7 @@ Adam (Keras ``Adam`` / TF ``ResourceApplyAdam``, beta1 .9, beta2 .999, epsilon 1
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, Optional
+from typing import Callable, Dict, Optional
 
 import numpy as np
 
@@ -153,6 +153,59 @@ def adam_step(theta, m, v, grad, step: int, dp: DQNParams = DQNParams()):
     theta -= (m * lr_t) / (np.sqrt(v) + F32(dp.adam_eps))
 
 
+RED_SLICES = 16  # dqn_reduce_adam_kernel: 16 waves per parameter fold a segment's partials
+
+
+def block_layout(n_agents: int, segments: int = 1, agents_per_block: int = 0):
+    """The shared network's gradient layout (p2pmg_dqn_setup, include/p2pmg.h grad_segments): the
+    agents split into `segments` contiguous segments, each into blocks of `agents_per_block` agents
+    (0: one block per segment here; the device's automatic choice depends on its CU count).
+    Returns (seg_agents, apb, bps, [(first agent, count)] per block in launch order)."""
+    if n_agents % segments:
+        raise ValueError("grad_segments must divide the agents (whole scenarios)")
+    seg_agents = n_agents // segments
+    apb = agents_per_block if agents_per_block > 0 else seg_agents
+    bps = -(-seg_agents // apb)
+    blocks = []
+    for g in range(segments):
+        for j in range(bps):
+            a0 = g * seg_agents + j * apb
+            blocks.append((a0, min(apb, (g + 1) * seg_agents - a0)))
+    return seg_agents, apb, bps, blocks
+
+
+def fold_segments(partials, bps: int):
+    """dqn_reduce_adam_kernel's order for each segment (rows of `partials` [segments * bps, P]):
+    16 slices of ceil(bps / 16) consecutive partials, each summed from +0.0 in partial order, then
+    slice 0 + slice 1 + ... + slice 15.  Returns [segments, P] float32."""
+    partials = np.asarray(partials, F32)
+    n_seg = partials.shape[0] // bps
+    per = -(-bps // RED_SLICES)
+    out = np.zeros((n_seg, partials.shape[1]), F32)
+    for g in range(n_seg):
+        blk = partials[g * bps:(g + 1) * bps]
+        parts = []
+        for sl in range(RED_SLICES):
+            acc = np.zeros(partials.shape[1], F32)
+            for b in range(sl * per, min(bps, sl * per + per)):
+                acc = acc + blk[b]
+            parts.append(acc)
+        t = parts[0]
+        for r in range(1, RED_SLICES):
+            t = t + parts[r]
+        out[g] = t
+    return out
+
+
+def sum_segments(segs):
+    """dqn_adam_shared_kernel: the segments of every rank summed in global segment order."""
+    segs = np.asarray(segs, F32)
+    t = segs[0].copy()
+    for g in range(1, segs.shape[0]):
+        t = t + segs[g]
+    return t
+
+
 def soft_update(target, theta, tau: float):
     """Trainer._soft_update (rl.py:335-354) with tau != 1: t <- (1 - tau) * t + tau * w."""
     target[...] = (F32(1) - F32(tau)) * target + F32(tau) * theta
@@ -199,6 +252,13 @@ class OracleDQNBatch:
     params: OracleParams = field(default_factory=OracleParams)
     dqn: DQNParams = field(default_factory=DQNParams)
     price_table: Optional[tuple] = None
+    # shared network: the gradient layout (p2pmg_dqn_config) and, over several ranks, the host
+    # all-gather of every rank's segments ([world, segments * P] rows, this rank's filled in)
+    agents_per_block: int = 0
+    grad_segments: int = 1
+    rank: int = 0
+    world: int = 1
+    exchange: Optional[Callable] = None
 
     def __post_init__(self):
         self.T = self.load_w.shape[-1]
@@ -225,6 +285,26 @@ class OracleDQNBatch:
             self.buy, self.inj, self.p2p = prices(self.env_time, p)
         else:
             self.buy, self.inj, self.p2p = (np.asarray(x, F32).reshape(-1, T) for x in self.price_table)
+
+    def _shared_gradient(self, gr):
+        """Mean gradient of every agent of every rank in the device's summation structure: block
+        partials (agents in order), each segment folded by fold_segments, every rank's segments
+        gathered (exchange) and summed in global order, times 1 / (agents over all ranks)."""
+        A = gr.shape[0]
+        _, _, bps, blocks = block_layout(A, self.grad_segments, self.agents_per_block)
+        partials = np.zeros((len(blocks), N_PARAMS), F32)
+        for k, (a0, n) in enumerate(blocks):
+            acc = np.zeros(N_PARAMS, F32)
+            for a in range(a0, a0 + n):
+                acc = acc + gr[a]
+            partials[k] = acc
+        segs = fold_segments(partials, bps)
+        if self.world > 1:
+            rows = np.zeros((self.world, segs.size), F32)
+            rows[self.rank] = segs.ravel()
+            self.exchange(rows)
+            segs = rows.reshape(-1, N_PARAMS)
+        return sum_segments(segs) * (F32(1) / F32(A * self.world))
 
     def _env(self, arr, t):
         return arr[:, t] if arr.shape[0] == self.S else np.broadcast_to(arr[0, t], (self.S,))
@@ -318,10 +398,7 @@ class OracleDQNBatch:
                     gr, ls = gradients(np.broadcast_to(self.theta[0], (A, N_PARAMS)), b[..., 0:4], b[..., 4],
                                        b[..., 5], b[..., 6:10], np.broadcast_to(self.target[0], (A, N_PARAMS)),
                                        dp.gamma, dp.clip)
-                    gsum = np.zeros(N_PARAMS, F32)
-                    for k in range(A):                                     # canonical agent order
-                        gsum = gsum + gr[k]
-                    adam_step(self.theta, self.m, self.v, (gsum / F32(A))[None], self.step, dp)
+                    adam_step(self.theta, self.m, self.v, self._shared_gradient(gr)[None], self.step, dp)
                 else:
                     gr, ls = gradients(self.theta, b[..., 0:4], b[..., 4], b[..., 5], b[..., 6:10], self.target,
                                        dp.gamma, dp.clip)

@@ -73,14 +73,26 @@ def _build_locked(obj_dir: str, out: str, defines, jobs: int, verbose: bool) -> 
     pending = list(units)
     running = []
     objs = []
+    # an object newer than its source, every header and this script is reused (same tag = same flags)
+    hdrs = [h if os.path.isabs(h) else os.path.join(CSRC, h) for h in HEADERS] + [os.path.abspath(__file__)]
+    newest_hdr = max(os.path.getmtime(h) for h in hdrs if os.path.exists(h))
+
+    def fresh(src, obj):
+        return os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), newest_hdr)
+
     while pending or running:
         while pending and len(running) < jobs:
             src, extra, o = pending.pop(0)
+            if fresh(src, os.path.join(obj_dir, o)):
+                objs.append(os.path.join(obj_dir, o))
+                continue
             cmd = [*common, *extra, "-c", src, "-o", os.path.join(obj_dir, o)]
             if verbose:
                 print(" ".join(cmd), flush=True)
             running.append((subprocess.Popen(cmd), cmd))
             objs.append(os.path.join(obj_dir, o))
+        if not running:
+            break
         proc, cmd = running.pop(0)
         if proc.wait() != 0:
             for q, _ in running:

@@ -39,7 +39,7 @@ EXPORTS = [
     "p2pmg_dqn_set_step", "p2pmg_dqn_get_step", "p2pmg_dqn_set_samples", "p2pmg_dqn_get_buffer",
     "p2pmg_dqn_set_buffer", "p2pmg_dqn_forward", "p2pmg_dqn_train_batch", "p2pmg_prepass_stats",
     "p2pmg_dqn_get_net_steps", "p2pmg_fdiv_check", "p2pmg_fdiv64_check", "p2pmg_comm_nranks",
-    "p2pmg_allreduce_metrics", "p2pmg_table_hash_allgather",
+    "p2pmg_allreduce_metrics", "p2pmg_table_hash_allgather", "p2pmg_dqn_set_exchange", "p2pmg_dqn_grad_layout",
 ]
 
 
@@ -61,10 +61,13 @@ class Config(C.Structure):
 class DqnConfig(C.Structure):
     _fields_ = [("gamma", C.c_double), ("tau", C.c_double), ("lr", C.c_double), ("beta1", C.c_double),
                 ("beta2", C.c_double), ("adam_eps", C.c_double), ("clip", C.c_double), ("batch", C.c_int32),
-                ("capacity", C.c_int32), ("agents_per_block", C.c_int32), ("reserved", C.c_int32)]
+                ("capacity", C.c_int32), ("agents_per_block", C.c_int32), ("grad_segments", C.c_int32)]
 
 
-ABI_VERSION = 5  # include/p2pmg.h P2PMG_ABI_VERSION
+ABI_VERSION = 6  # include/p2pmg.h P2PMG_ABI_VERSION
+
+# p2pmg_exchange_fn: int (*)(void* user, float* segments, int64_t floats_per_rank, int rank, int nranks)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_int64, C.c_int, C.c_int)
 
 
 class EpisodeArgs(C.Structure):
@@ -152,6 +155,8 @@ def _declare(lib):
         "p2pmg_comm_nranks": ([vp, C.POINTER(C.c_int)], i32),
         "p2pmg_allreduce_metrics": ([vp, vp], i32),
         "p2pmg_table_hash_allgather": ([vp, vp], i32),
+        "p2pmg_dqn_set_exchange": ([vp, EXCHANGE_FN, vp, i32, i32], i32),
+        "p2pmg_dqn_grad_layout": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

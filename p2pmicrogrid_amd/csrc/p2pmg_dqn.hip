@@ -795,7 +795,11 @@ __global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const D
   float gx1[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   float gb1 = 0.0f, gb3 = 0.0f;
   float gb2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gW3[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  const int n_ag = d.batch ? 1 : d.apb;
+  // this workgroup's run of agents: block j of gradient segment g covers agents g * seg_agents +
+  // j * apb .. (clipped to the segment), so no block straddles two segments (p2pmg_dqn_config)
+  const int seg = blockIdx.x / d.bps, sblk = blockIdx.x - seg * d.bps;
+  const int a_first = seg * d.seg_agents + sblk * d.apb;
+  const int n_ag = d.batch ? 1 : max(0, min(d.apb, (seg + 1) * d.seg_agents - a_first));
   int net = d.batch ? d.net : 0;
   TrainW W;
   // one shared network: the lane's 48 W2 operands (layer 2: W2[4 kk + g4][col] of the target and
@@ -816,9 +820,8 @@ __global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const D
   if (d.batch) {
     for (int k = threadIdx.x; k < kB * kTrans; k += 256) smpb[0][k] = d.batch[k];
   } else {
-    const int a0 = blockIdx.x * d.apb;
     float v0 = 0.0f, v1 = 0.0f;
-    if ((size_t)a0 < A) batch_part(d, a0, threadIdx.x, v0, v1);
+    if (n_ag > 0) batch_part(d, a_first, threadIdx.x, v0, v1);
     batch_put(smpb[0], threadIdx.x, v0, v1);
   }
   // the next agent's slot index, loaded one agent ahead of its transitions: the dependent pair of
@@ -827,7 +830,7 @@ __global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const D
   // loop-carried register copy that waits for every load in flight)
   const int a_last = (int)A - 1;
   const int tag4 = reduce4_tag();
-  int slot_n = batch_slot(d, min((int)(blockIdx.x * d.apb) + 1, a_last), threadIdx.x);
+  int slot_n = batch_slot(d, min(a_first + 1, a_last), threadIdx.x);
   __syncthreads();
 
 #if P2PMG_TRACE
@@ -835,15 +838,14 @@ __global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const D
   asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(tlast)::"memory");
 #endif
   for (int ag = 0; ag < n_ag; ++ag) {
-    const int a = d.batch ? 0 : blockIdx.x * d.apb + ag;
-    if (!d.batch && a >= (int)A) break;  // block-uniform
+    const int a = d.batch ? 0 : a_first + ag;
     net = d.batch ? d.net : (SHARED ? 0 : a);
     const float* th = d.theta + (size_t)net * kNetStride;
     const float* tg = d.target + (size_t)net * kNetStride;
     if (!SHARED) load_train_w(W, th, tg, col, g4, h0);
     float (*smp)[kTrans] = reinterpret_cast<float (*)[kTrans]>(smpb[ag & 1]);
     // prefetch the next agent's batch into registers; it goes to the other buffer at the end
-    const bool has_next = !d.batch && ag + 1 < n_ag && a + 1 < (int)A;
+    const bool has_next = !d.batch && ag + 1 < n_ag;
     float nx0, nx1;
     batch_part_at(d, min(a + 1, a_last), threadIdx.x, (int)min((unsigned)slot_n, (unsigned)(d.cap - 1)), nx0, nx1);
     slot_n = batch_slot(d, min(a + 2, a_last), threadIdx.x);
@@ -1127,16 +1129,18 @@ __global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const D
   }
 }
 
-// shared network, one launch: the partials' sum and (adam != 0) the Adam step.  A 1024-thread
-// workgroup owns 64 parameters; its 16 waves each fold a contiguous run of the partials in partial
-// order (8 loads in flight), and wave 0 adds the 16 runs in run order — a fixed order, so every
-// launch gives the same sum.  adam == 0 leaves the sum in gsum for the cross-rank all-reduce.
+// shared network: each gradient segment's sum of its train workgroups' partials (blockIdx.y = the
+// local segment).  A 1024-thread workgroup owns 64 parameters; its 16 waves each fold a contiguous
+// run of the segment's partials in partial order (8 loads in flight), and wave 0 adds the 16 runs
+// in run order: a fixed order that depends only on the segment's block count, so a segment gives the
+// same sum on any rank and in any launch.  adam != 0 (one segment over every rank): the Adam step
+// on that sum in the same launch; else the sum goes to segs[seg_first + segment] for the gather.
 constexpr int kRedParams = 64, kRedSlices = 16;
-__global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kernel(const DqnParams d, int n_partials,
-                                                                               int adam) {
+__global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kernel(const DqnParams d, int adam) {
   __shared__ float part[kRedSlices][kRedParams];
   const int j = threadIdx.x % kRedParams, sl = threadIdx.x / kRedParams;
   const int k = blockIdx.x * kRedParams + j;
+  const int n_partials = d.bps;
   const int per = (n_partials + kRedSlices - 1) / kRedSlices;
   const int b0 = sl * per, b1 = min(n_partials, b0 + per);
   // the Adam state of this parameter, loaded ahead of the partials (one memory round trip less)
@@ -1149,7 +1153,7 @@ __global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kerne
   }
   float s = 0.0f;
   if (k < kDqnParams) {
-    const float* g = d.grad + k;
+    const float* g = d.grad + (size_t)blockIdx.y * n_partials * kNetStride + k;
     int b = b0;
     for (; b + 8 <= b1; b += 8) {
       float v[8];
@@ -1167,7 +1171,7 @@ __global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kerne
 #pragma unroll
   for (int r = 1; r < kRedSlices; ++r) t += part[r][j];
   if (!adam) {
-    d.gsum[k] = t;
+    d.segs[(size_t)(d.seg_first + blockIdx.y) * kNetStride + k] = t;
     return;
   }
   float gk = t * d.inv_agents;
@@ -1182,13 +1186,16 @@ __global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kerne
   d.target[k] = d.tau_c * tg0 + d.tau * w0;
 }
 
-// shared network: mean over every agent (all ranks after the all-reduce), clip, Adam, soft update
+// shared network over several segments / ranks: the segments' sum in global segment order, the mean
+// over every agent of every rank, clip, Adam, soft update (every rank computes the same values)
 __global__ void dqn_adam_shared_kernel(const DqnParams d) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= kDqnParams) return;
-  float g = d.gsum[k] * d.inv_agents;
-  if (k < kOffB1) g = fminf(fmaxf(g, -d.clip), d.clip);
-  adam_update(d, d.theta, d.target, d.adam_m, d.adam_v, k, g, d.lr_t);
+  float t = d.segs[k];
+  for (int g = 1; g < d.n_segs; ++g) t += d.segs[(size_t)g * kNetStride + k];
+  float gk = t * d.inv_agents;
+  if (k < kOffB1) gk = fminf(fmaxf(gk, -d.clip), d.clip);
+  adam_update(d, d.theta, d.target, d.adam_m, d.adam_v, k, gk, d.lr_t);
 }
 
 // QNetwork.call on explicit rows (object API, rl.py:147-148): one thread per row
@@ -1266,9 +1273,10 @@ hipError_t launch_dqn_sample(const DqnParams& d, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_dqn_reduce_adam(const DqnParams& d, int n_partials, bool adam, hipStream_t st) {
-  hipLaunchKernelGGL(dqn_reduce_adam_kernel, dim3((kDqnParams + kRedParams - 1) / kRedParams),
-                     dim3(kRedParams * kRedSlices), 0, st, d, n_partials, adam ? 1 : 0);
+hipError_t launch_dqn_reduce_adam(const DqnParams& d, int segments, bool adam, hipStream_t st) {
+  if (segments < 1 || d.bps < 1 || (adam && segments != 1)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dqn_reduce_adam_kernel, dim3((kDqnParams + kRedParams - 1) / kRedParams, segments),
+                     dim3(kRedParams * kRedSlices), 0, st, d, adam ? 1 : 0);
   return hipGetLastError();
 }
 

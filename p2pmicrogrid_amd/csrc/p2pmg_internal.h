@@ -80,8 +80,12 @@ struct DqnParams {
   float* target;             // [n_nets][kNetStride] target network
   float* adam_m;
   float* adam_v;
-  float* grad;               // shared: [blocks][kNetStride] partial sums; then the sum in row 0 of gsum
-  float* gsum;               // shared: [kNetStride]
+  float* grad;               // shared: [blocks][kNetStride] train-workgroup partial sums
+  float* segs;               // shared: [n_segs][kNetStride] gradient segments of every rank (global order)
+  int seg_first;             // global index of this context's first segment
+  int n_segs;                // segments over every rank
+  int seg_agents;            // agents per segment (a segment is whole scenarios)
+  int bps;                   // train workgroups per segment: ceil(seg_agents / apb)
   float* buf;                // [A][cap][kTrans] replay rings
   int32_t* added;            // [A] transitions ever added
   int cap;
@@ -103,8 +107,10 @@ hipError_t launch_dqn_act(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_sample(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_train(const DqnParams& p, int blocks, bool shared_partials, hipStream_t stream);
 int dqn_train_blocks_per_cu();  // train workgroups resident per CU (the build's occupancy target)
-// sum of the train workgroups' partials (+ adam: the Adam step on it; else the sum goes to gsum)
-hipError_t launch_dqn_reduce_adam(const DqnParams& p, int n_partials, bool adam, hipStream_t stream);
+// each local segment's sum of its train-workgroup partials -> segs[seg_first + j] (segments = local
+// segment count); adam (one segment over every rank): the Adam step on it directly
+hipError_t launch_dqn_reduce_adam(const DqnParams& p, int segments, bool adam, hipStream_t stream);
+// sum of the n_segs segments in global order, then mean, clip, Adam, soft update
 hipError_t launch_dqn_adam_shared(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_forward(const float* theta, int n, const float* x, float* q, hipStream_t stream);
 

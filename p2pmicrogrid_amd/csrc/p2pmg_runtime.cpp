@@ -39,6 +39,7 @@ struct p2pmg_ctx {
   static constexpr int kCRing = 1024;
   std::vector<hipEvent_t> cring;  // 2 * kCRing events: start/stop of each data-path RCCL all-reduce
   long long n_coll = 0;           // collectives recorded since the last reset
+  double coll_folded_ms = 0.0;    // durations of ring slots already reused (p2pmg_collective_ms)
   int timing_period = 1;          // episode launches: stamp timing events on every k-th one
   long long n_launch = 0;         // episode launches since the last reset
   // device buffers
@@ -87,7 +88,9 @@ struct p2pmg_ctx {
   double bat_min = 0.1, bat_max = 0.9, bat_sqrt_eff = 1.0;
   long long* qdelta = nullptr; // shared table deltas [kDeltaCopies][n_states][4]
   void* comm = nullptr;        // ncclComm_t
-  int nranks = 1;
+  int rank = 0, nranks = 1;    // this context's rank and the world (RCCL communicator or DQN host exchange)
+  p2pmg_exchange_fn xfn = nullptr;  // DQN shared network: host gather of the gradient segments
+  void* xuser = nullptr;
   double* d_metrics = nullptr;           // [2] episode-metric sum and count (p2pmg_allreduce_metrics)
   unsigned long long* d_hash = nullptr;  // [nranks] table fingerprints (p2pmg_table_hash_allgather)
   bool have_env = false, have_prof = false, have_params = false, have_codes = false;
@@ -100,9 +103,13 @@ struct p2pmg_ctx {
   float* d_m = nullptr;
   float* d_v = nullptr;
   float* d_grad = nullptr;    // shared network: [d_blocks][kNetStride] partials
-  float* d_gsum = nullptr;    // [kNetStride]
+  float* d_segs = nullptr;    // [nranks * d_seg_local][kNetStride] gradient segments, global order
+  size_t d_segs_cap = 0;      // floats at d_segs
+  float* h_segs = nullptr;    // pinned host copy of d_segs (host exchange)
+  size_t h_segs_cap = 0;
   float* d_smp = nullptr;     // [A][32] int32 ring slots sampled for the current step
   int d_blocks = 0, d_apb = 1;
+  int d_seg_local = 1, d_seg_agents = 0, d_bps = 0;  // gradient segments of this context (p2pmg_dqn_config)
   float* d_buf = nullptr;     // [A][capacity][10]
   int32_t* d_added = nullptr; // [A]
   uint16_t* d_samples = nullptr;  // [T][A][32]
@@ -363,7 +370,8 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   dfree(c->d_v);
   dfree(c->d_lr);
   dfree(c->d_grad);
-  dfree(c->d_gsum);
+  dfree(c->d_segs);
+  if (c->h_segs) (void)hipHostFree(c->h_segs);
   dfree(c->d_smp);
   dfree(c->d_buf);
   dfree(c->d_added);
@@ -886,6 +894,7 @@ int p2pmg_reset_kernel_times(p2pmg_ctx* c) {
   c->n_timed = 0;
   c->n_launch = 0;
   c->n_coll = 0;
+  c->coll_folded_ms = 0.0;
   return P2PMG_OK;
 }
 
@@ -1147,6 +1156,7 @@ int p2pmg_comm_init(p2pmg_ctx* c, const uint8_t id[128], int rank, int nranks) {
   const int rc = r->commInitRank(&comm, nranks, uid, rank);
   if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclCommInitRank: ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
   c->comm = comm;
+  c->rank = rank;
   c->nranks = nranks;
   return P2PMG_OK;
 }
@@ -1162,6 +1172,15 @@ static hipError_t coll_mark(p2pmg_ctx* c, int end) {
     }
   }
   const int slot = (int)(c->n_coll % p2pmg_ctx::kCRing);
+  if (!end && c->n_coll >= p2pmg_ctx::kCRing) {
+    // the slot's previous pair (kCRing collectives ago) is about to be overwritten: fold its
+    // duration into the running total first, so p2pmg_collective_ms counts every collective
+    float ms = 0.0f;
+    hipError_t e = hipEventSynchronize(c->cring[2 * slot + 1]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->cring[2 * slot], c->cring[2 * slot + 1]);
+    if (e != hipSuccess) return e;
+    c->coll_folded_ms += ms;
+  }
   const hipError_t e = hipEventRecord(c->cring[2 * slot + end], c->stream);
   if (end) c->n_coll++;
   return e;
@@ -1178,8 +1197,8 @@ int p2pmg_collective_ms(p2pmg_ctx* c, double* total_ms, int* count) {
     HIP_TRY(c, hipEventElapsedTime(&ms, c->cring[2 * slot], c->cring[2 * slot + 1]));
     sum += ms;
   }
-  *total_ms = sum;
-  *count = (int)n;
+  *total_ms = c->coll_folded_ms + sum;
+  *count = (int)c->n_coll;
   return P2PMG_OK;
 }
 
@@ -1250,6 +1269,7 @@ int p2pmg_comm_destroy(p2pmg_ctx* c) {
   if (!c) return P2PMG_E_INVALID;
   if (c->comm && rccl()) rccl()->commDestroy(c->comm);
   c->comm = nullptr;
+  if (!c->xfn) c->rank = 0, c->nranks = 1;
   return P2PMG_OK;
 }
 
@@ -1348,17 +1368,26 @@ int p2pmg_dqn_setup(p2pmg_ctx* c, const p2pmg_dqn_config* cfg) {
   HIP_TRY(c, dmalloc(&c->d_m, nn));
   HIP_TRY(c, dmalloc(&c->d_v, nn));
   for (float* b : {c->d_theta, c->d_target, c->d_m, c->d_v}) HIP_TRY(c, hipMemsetAsync(b, 0, nn * 4, c->stream));
+  if (cfg->agents_per_block < 0 || cfg->grad_segments < 0) return fail(c, P2PMG_E_INVALID, "dqn_setup: negative layout");
   if (c->cfg.shared_q) {
+    // gradient segments: contiguous runs of whole scenarios; the train workgroups never straddle two
+    const int G = cfg->grad_segments > 0 ? cfg->grad_segments : 1;
+    if (c->S % G) return fail(c, P2PMG_E_INVALID, "dqn_setup: grad_segments must divide the scenarios");
+    c->d_seg_local = G;
+    c->d_seg_agents = c->A / G;
     // default: one wave of train workgroups (2 per CU in the default build: 512 on 256 CUs)
     const size_t slots = (size_t)c->n_cu * (size_t)p2pmg::dqn_train_blocks_per_cu();
     int apb = cfg->agents_per_block > 0 ? cfg->agents_per_block : (int)((A + slots - 1) / slots);
     c->d_apb = apb < 1 ? 1 : apb;
-    c->d_blocks = (int)((A + c->d_apb - 1) / c->d_apb);
+    c->d_bps = (c->d_seg_agents + c->d_apb - 1) / c->d_apb;
+    c->d_blocks = G * c->d_bps;
     HIP_TRY(c, dmalloc(&c->d_grad, (size_t)c->d_blocks * NS));
-    HIP_TRY(c, dmalloc(&c->d_gsum, NS));
   } else {
     c->d_apb = 1;
     c->d_blocks = c->A;
+    c->d_seg_local = 1;
+    c->d_seg_agents = c->A;
+    c->d_bps = c->A;
   }
   HIP_TRY(c, dmalloc(&c->d_buf, A * (size_t)cfg->capacity * p2pmg::kTrans));
   HIP_TRY(c, dmalloc(&c->d_added, A));
@@ -1496,7 +1525,11 @@ static p2pmg::DqnParams dqn_params(p2pmg_ctx* c, const EpisodeParams& e) {
   d.adam_v = c->d_v;
   d.grad = c->d_grad;
   d.smp = c->d_smp;
-  d.gsum = c->d_gsum;
+  d.segs = c->d_segs;
+  d.seg_first = c->rank * c->d_seg_local;
+  d.n_segs = c->nranks * c->d_seg_local;
+  d.seg_agents = c->d_seg_agents;
+  d.bps = c->d_bps;
   d.buf = c->d_buf;
   d.added = c->d_added;
   d.cap = q.capacity;
@@ -1547,6 +1580,54 @@ static int dqn_upload_lr_table(p2pmg_ctx* c) {
   return P2PMG_OK;
 }
 
+// The shared network's gradient segments of every rank in d_segs ([nranks * d_seg_local][kNetStride]),
+// allocated for the current world (comm_init / set_exchange may come after dqn_setup)
+static int dqn_ensure_segs(p2pmg_ctx* c, p2pmg::DqnParams& d) {
+  const size_t need = (size_t)c->nranks * c->d_seg_local * p2pmg::kNetStride;
+  if (c->d_segs_cap < need) {
+    dfree(c->d_segs);
+    c->d_segs_cap = 0;
+    HIP_TRY(c, dmalloc(&c->d_segs, need));
+    c->d_segs_cap = need;
+  }
+  if (c->xfn && !c->comm && c->h_segs_cap < need) {
+    if (c->h_segs) (void)hipHostFree(c->h_segs);
+    c->h_segs = nullptr;
+    c->h_segs_cap = 0;
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_segs), need * 4, hipHostMallocDefault));
+    c->h_segs_cap = need;
+  }
+  d.segs = c->d_segs;
+  d.seg_first = c->rank * c->d_seg_local;
+  d.n_segs = c->nranks * c->d_seg_local;
+  return P2PMG_OK;
+}
+
+// every rank's segments into d_segs: RCCL all-gather in place (xGMI), or the host exchange function
+static int dqn_gather_segments(p2pmg_ctx* c) {
+  const size_t per = (size_t)c->d_seg_local * p2pmg::kNetStride;  // floats per rank
+  if (c->comm) {
+    Rccl* r = rccl();
+    if (!r->allGather) return fail(c, P2PMG_E_UNSUPPORTED, "ncclAllGather not found");
+    // ncclFloat32 = 7; in place: this rank's part already sits at d_segs + rank * per
+    HIP_TRY(c, coll_mark(c, 0));
+    const int rc = r->allGather(c->d_segs + (size_t)c->rank * per, c->d_segs, per, 7, c->comm, c->stream);
+    if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("dqn gradient all-gather: ") +
+                                                 (r->getErrorString ? r->getErrorString(rc) : "?"));
+    HIP_TRY(c, coll_mark(c, 1));
+    return P2PMG_OK;
+  }
+  if (!c->xfn) return fail(c, P2PMG_E_STATE, "dqn: several ranks but neither a communicator nor an exchange");
+  float* own = c->h_segs + (size_t)c->rank * per;
+  HIP_TRY(c, hipMemcpyAsync(own, c->d_segs + (size_t)c->rank * per, per * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (c->xfn(c->xuser, c->h_segs, (int64_t)per, c->rank, c->nranks) != 0)
+    return fail(c, P2PMG_E_STATE, "dqn: the host gradient exchange failed");
+  HIP_TRY(c, hipMemcpyAsync(c->d_segs, c->h_segs, (size_t)c->nranks * per * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));  // h_segs is rewritten by the next env step
+  return P2PMG_OK;
+}
+
 static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
   // one env step trains every network once (community.py:158-168)
   for (auto& st : c->d_steps) ++st;
@@ -1555,15 +1636,14 @@ static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
   if (!d.fused_sample) HIP_TRY(c, p2pmg::launch_dqn_sample(d, c->stream));
   if (c->n_nets == 1) {
     HIP_TRY(c, p2pmg::launch_dqn_train(d, c->d_blocks, true, c->stream));
-    const bool ranks = c->comm && c->nranks > 1;
-    HIP_TRY(c, p2pmg::launch_dqn_reduce_adam(d, c->d_blocks, !ranks, c->stream));  // one rank: sum + Adam
-    if (ranks) {
-      Rccl* r = rccl();
-      // ncclFloat32 = 7, ncclSum = 0: gradient sum over ranks (xGMI), 4609 floats
-      HIP_TRY(c, coll_mark(c, 0));
-      const int rc = r->allReduce(c->d_gsum, c->d_gsum, p2pmg::kDqnParams, 7, 0, c->comm, c->stream);
-      if (rc != 0) return fail(c, P2PMG_E_HIP, "dqn gradient all-reduce failed");
-      HIP_TRY(c, coll_mark(c, 1));
+    if (c->nranks == 1 && c->d_seg_local == 1) {  // one segment in all: its sum + Adam in one launch
+      HIP_TRY(c, p2pmg::launch_dqn_reduce_adam(d, 1, true, c->stream));
+    } else {
+      HIP_TRY(c, p2pmg::launch_dqn_reduce_adam(d, c->d_seg_local, false, c->stream));
+      if (c->nranks > 1) {
+        const int rc = dqn_gather_segments(c);
+        if (rc != P2PMG_OK) return rc;
+      }
       HIP_TRY(c, p2pmg::launch_dqn_adam_shared(d, c->stream));
     }
   } else {
@@ -1594,6 +1674,10 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   e.rng = (acting && args->rng == P2PMG_RNG_PHILOX) ? 1 : 0;
   p2pmg::DqnParams d = dqn_params(c, e);
   if (mode == P2PMG_MODE_TRAIN && args->rng == P2PMG_RNG_REPLAY) d.samples = c->d_samples;
+  if (mode == P2PMG_MODE_TRAIN && c->n_nets == 1 && (c->nranks > 1 || c->d_seg_local > 1)) {
+    rc = dqn_ensure_segs(c, d);
+    if (rc != P2PMG_OK) return rc;
+  }
   if (c->ring.empty()) {
     c->ring.assign(2 * p2pmg_ctx::kRing, nullptr);
     for (auto& ev : c->ring) HIP_TRY(c, hipEventCreate(&ev));
@@ -1668,6 +1752,33 @@ int p2pmg_dqn_train_batch(p2pmg_ctx* c, int net, const float* batch, float* loss
   dfree(db);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("dqn_train_batch: ") + hipGetErrorString(e));
   if (loss) *loss = l;
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_set_exchange(p2pmg_ctx* c, p2pmg_exchange_fn fn, void* user, int rank, int nranks) {
+  if (!c) return P2PMG_E_INVALID;
+  if (c->comm) return fail(c, P2PMG_E_STATE, "dqn_set_exchange: the context has an RCCL communicator");
+  if (!fn) {
+    c->xfn = nullptr;
+    c->xuser = nullptr;
+    c->rank = 0;
+    c->nranks = 1;
+    return P2PMG_OK;
+  }
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(c, P2PMG_E_INVALID, "dqn_set_exchange: rank / nranks");
+  c->xfn = fn;
+  c->xuser = user;
+  c->rank = rank;
+  c->nranks = nranks;
+  return P2PMG_OK;
+}
+
+int p2pmg_dqn_grad_layout(p2pmg_ctx* c, int* segments, int* agents_per_block, int* blocks) {
+  int rc = dqn_ready(c, "dqn_grad_layout");
+  if (rc != P2PMG_OK) return rc;
+  if (segments) *segments = c->d_seg_local;
+  if (agents_per_block) *agents_per_block = c->d_apb;
+  if (blocks) *blocks = c->d_blocks;
   return P2PMG_OK;
 }
 

@@ -12,6 +12,13 @@ rank accumulates its scenarios' TD deltas in int64 fixed point, the deltas are s
 ranks once per episode (RCCL all-reduce on the device stream, or a host-side sum over the
 process group), and each rank applies the identical sum.  Integer addition is associative, so
 the table after each episode is bit-identical for every world size.
+
+With ONE shared DQN network (config 5, ``learner="dqn"``) the exchange is per env step: every
+rank sums its agents' gradients into fixed gradient segments (contiguous runs of whole scenarios,
+each folded in a fixed block order), the segments of all ranks are gathered (RCCL all-gather on the
+device stream, or a host all-gather over the process group) and every rank adds them in global
+segment order before the same Adam step.  With the total segment count and the agents per block
+fixed, 1 rank x G segments and W ranks x G/W segments give the same weights bit for bit.
 """
 from __future__ import annotations
 
@@ -72,6 +79,21 @@ def all_reduce_int64(values: np.ndarray, world: int) -> np.ndarray:
     return t.numpy()
 
 
+def all_gather_rows(rows: np.ndarray, rank: int, world: int) -> None:
+    """In-place all-gather of a [world, n] float32 array whose row `rank` is filled in (the host
+    exchange of the DQN gradient segments), over the torch process group."""
+    if world == 1:
+        return
+    import torch
+    import torch.distributed as dist
+    mine = torch.from_numpy(np.ascontiguousarray(rows[rank]))
+    out = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(out, mine)
+    for r in range(world):
+        if r != rank:
+            rows[r] = out[r].numpy()
+
+
 def broadcast_bytes(data: Optional[bytes], world: int, src: int = 0) -> bytes:
     if world == 1:
         return data
@@ -92,36 +114,60 @@ def all_gather_concat(values: np.ndarray, world: int) -> np.ndarray:
 
 
 class ShardedTrainer:
-    """Tabular training of S_total scenarios sharded over the ranks.
+    """Training of S_total scenarios sharded over the ranks: tabular Q-learning (the reference's
+    QAgent) or, with learner="dqn", DQN agents sharing ONE Q-network (config 5).
 
-    engine_factory(shard, S, N, R, T, q_dtype, device, seed, shared_q) -> an object with the
-    DeviceCommunityBatch interface; the default is the HIP engine.
+    engine_factory(shard, S, N, R, T, q_dtype, device, seed, shared_q, **dqn) -> an object with the
+    DeviceCommunityBatch (DeviceDQNBatch) interface; the default is the HIP engine.
 
     shared_q: one policy table for every agent of every scenario on every rank (config 3).
     exchange: how the shared-table deltas and the episode metrics are summed over ranks — "rccl"
     (device all-reduce over xGMI through the context's RCCL communicator, the production path),
     "host" (copy out, sum over the torch process group, copy back) or "auto" (rccl when the
     process group is nccl/RCCL, host otherwise).
-    battery: kwargs for ``set_battery`` (scalars), enabling the storage rule."""
+    battery: kwargs for ``set_battery`` (scalars), enabling the storage rule.
+    learner="dqn": grad_segments = the TOTAL gradient segment count (default: one per rank; must be
+    a multiple of world and divide n_scenarios) and agents_per_block fix the gradient's summation
+    structure, so a run is bit-identical for every world size that divides grad_segments; the
+    gradient exchange ("rccl" | "host") runs once per env step."""
 
     def __init__(self, n_scenarios: int, n_agents: int = 2, rounds: int = 1, horizon: int = 96,
                  q_dtype: str = "f64", seed: int = 42, rank: int = 0, world: int = 1, device: int = 0,
                  engine_factory: Optional[Callable] = None, shared_q: bool = False, exchange: str = "auto",
-                 battery: Optional[dict] = None, homogeneous: bool = False):
+                 battery: Optional[dict] = None, homogeneous: bool = False, learner: str = "tabular",
+                 grad_segments: Optional[int] = None, agents_per_block: int = 0):
         from .dataset import scenario_batch
+        if learner not in ("tabular", "dqn"):
+            raise ValueError(f"learner must be 'tabular' or 'dqn', got {learner!r}")
+        self.learner = learner
+        dqn_kw = {}
+        if learner == "dqn":
+            G = world if grad_segments is None else int(grad_segments)
+            if G < 1 or G % world or n_scenarios % G:
+                raise ValueError(f"grad_segments={G} must be a multiple of world={world} and divide "
+                                 f"n_scenarios={n_scenarios}")
+            self.grad_segments = G
+            dqn_kw = dict(learner="dqn", grad_segments=G // world, agents_per_block=agents_per_block)
+            shared_q = True
+            self.filled = False
         self.sh = shard(n_scenarios, rank, world)
         self.S_total, self.N, self.R, self.T = n_scenarios, n_agents, rounds, horizon
         self.rank, self.world, self.shared_q = rank, world, bool(shared_q)
         inp = scenario_batch(self.sh.count, n_agents, horizon, seed=seed, first_scenario=self.sh.first,
                              homogeneous=homogeneous)
         if engine_factory is None:
-            from .engine import DeviceCommunityBatch
-
-            def engine_factory(sh, S, N, R, T, q_dtype, device, seed, shared_q=False):
+            def engine_factory(sh, S, N, R, T, q_dtype, device, seed, shared_q=False, learner="tabular",
+                               grad_segments=1, agents_per_block=0):
+                if learner == "dqn":
+                    from .dqn import DeviceDQNBatch
+                    return DeviceDQNBatch(S, N, R, T, shared=True, device=device, seed=seed, scenario_offset=sh.first,
+                                          grad_segments=grad_segments, agents_per_block=agents_per_block, init_seed=0)
+                from .engine import DeviceCommunityBatch
                 return DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=device, seed=seed,
                                             scenario_offset=sh.first, shared_q=shared_q)
+        self.shared_q = bool(shared_q)
         self.eng = engine_factory(self.sh, self.sh.count, n_agents, rounds, horizon, q_dtype, device, seed,
-                                  shared_q=self.shared_q)
+                                  shared_q=self.shared_q, **dqn_kw)
         self.eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
         self.eng.set_profiles(inp.load_w, inp.pv_w)
         self.eng.set_max_in(inp.max_in)
@@ -139,6 +185,8 @@ class ShardedTrainer:
                 from .engine import comm_unique_id
                 uid = broadcast_bytes(comm_unique_id() if rank == 0 else None, world)
                 self.eng.comm_init(uid, rank, world)
+            elif learner == "dqn":  # the per-env-step gradient gather, over the process group
+                self.eng.set_grad_exchange(lambda rows: all_gather_rows(rows, rank, world), rank, world)
             self.exchange = exchange
         self.episode = 0
 
@@ -150,20 +198,41 @@ class ShardedTrainer:
             self.eng.set_q_delta(all_reduce_int64(self.eng.get_q_delta(), self.world))
         self.eng.apply_q_delta()
 
+    def fill_buffers(self, episodes: int = 1, reset_sigma: float = 0.3):
+        """DQN: CommunityMicrogrid.init_buffers (community.py:125-147): episodes of acting at
+        epsilon 1 that only store transitions (>= 31 per agent before training can start)."""
+        for _ in range(episodes):
+            self.eng.run_episode("fill", "philox", episode=self.episode, epsilon=1.0)
+            self.eng.reset_temperatures_philox(self.episode + 1, reset_sigma)
+            self.episode += 1
+        self.filled = True
+
+    def _metrics(self):
+        if self.exchange == "rccl":  # episode metrics over RCCL, reduced on the device
+            return self.eng.allreduce_metrics()
+        local = self.eng.episode_reward().astype(np.float64)
+        return all_reduce_sum(np.array([local.sum(), local.size]), self.world)
+
     def train_episode(self, epsilon: float, reset_sigma: float = 0.3,
                       next_epsilon: Optional[float] = None) -> float:
         """One training episode on every shard; returns the global mean over scenarios of the
         episode reward (sum_t mean_i r, community.py:179).  next_epsilon: the next episode's
-        epsilon (the decay schedule, community.py:279-286), for the speculative pre-pass."""
+        epsilon (the decay schedule, community.py:279-286), for the speculative pre-pass.
+        DQN: the replay memory is filled first if it was not (fill_buffers); every env step's
+        gradient exchange happens inside the episode call."""
+        if self.learner == "dqn":
+            if not self.filled:
+                self.fill_buffers()
+            self.eng.run_episode("train", "philox", episode=self.episode, epsilon=epsilon)
+            total, count = self._metrics()
+            self.eng.reset_temperatures_philox(self.episode + 1, reset_sigma)
+            self.episode += 1
+            return float(total / count)
         self.eng.run_episode("train", "philox", episode=self.episode, epsilon=epsilon,
                              next_epsilon=next_epsilon)
         if self.shared_q:
             self.exchange_q_delta()
-        if self.exchange == "rccl":  # episode metrics over RCCL, reduced on the device
-            total, count = self.eng.allreduce_metrics()
-        else:
-            local = self.eng.episode_reward().astype(np.float64)
-            total, count = all_reduce_sum(np.array([local.sum(), local.size]), self.world)
+        total, count = self._metrics()
         self.eng.reset_temperatures_philox(self.episode + 1, reset_sigma)
         self.episode += 1
         return float(total / count)

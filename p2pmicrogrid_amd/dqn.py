@@ -50,18 +50,21 @@ class DeviceDQNBatch(DeviceCommunityBatch):
 
     def __init__(self, n_scenarios: int, n_agents: int, rounds: int, horizon: int, shared: bool = False,
                  device: int = 0, seed: int = 42, scenario_offset: int = 0, gamma: float = 0.95, tau: float = 0.005,
-                 lr: float = 1e-5, capacity: int = 5000, agents_per_block: int = 0,
+                 lr: float = 1e-5, capacity: int = 5000, agents_per_block: int = 0, grad_segments: int = 1,
                  init_seed: Optional[int] = 0, **overrides):
         super().__init__(n_scenarios, n_agents, rounds, horizon, q_dtype="f32", device=device, seed=seed,
                          scenario_offset=scenario_offset, shared_q=shared, learner=_lib.LEARNER_DQN, **overrides)
         dc = _lib.DqnConfig()
         _lib.check(self.L.p2pmg_dqn_config_default(C.byref(dc)), what="dqn_config_default")
         dc.gamma, dc.tau, dc.lr, dc.capacity, dc.agents_per_block = gamma, tau, lr, capacity, agents_per_block
+        dc.grad_segments = grad_segments
         self._chk(self.L.p2pmg_dqn_setup(self._ctx, C.byref(dc)), "dqn_setup")
         self.dcfg = dc
         self.shared = bool(shared)
         self.n_nets = 1 if shared else self.A
         self.capacity = capacity
+        self._xfn = None          # the host exchange's ctypes callback (kept alive while installed)
+        self._xerr = None
         if init_seed is not None:
             th = glorot_init(self.n_nets, init_seed)
             self.set_weights("online", th)
@@ -101,6 +104,37 @@ class DeviceDQNBatch(DeviceCommunityBatch):
         self._chk(self.L.p2pmg_dqn_get_net_steps(self._ctx, first, count, out.ctypes.data), "dqn_get_net_steps")
         return out
 
+    # ----------------------------------------------------------------- multi-rank shared network
+    def grad_layout(self) -> dict:
+        """Shared network: gradient segments of this context, agents per train workgroup, train
+        workgroups per env step (the summation structure the result depends on)."""
+        g, a, b = C.c_int(0), C.c_int(0), C.c_int(0)
+        self._chk(self.L.p2pmg_dqn_grad_layout(self._ctx, C.byref(g), C.byref(a), C.byref(b)), "dqn_grad_layout")
+        return {"segments": g.value, "agents_per_block": a.value, "blocks": b.value}
+
+    def set_grad_exchange(self, gather, rank: int, world: int):
+        """Host exchange of the shared network's gradient segments (no RCCL communicator):
+        ``gather(segs)`` gets the [world, floats_per_rank] f32 host array with this rank's row
+        filled in and must fill the other rows (an all-gather, e.g. over gloo); called once per
+        training env step from inside run_episode.  gather=None removes it."""
+        if gather is None:
+            self._chk(self.L.p2pmg_dqn_set_exchange(self._ctx, _lib.EXCHANGE_FN(), None, 0, 1), "dqn_set_exchange")
+            self._xfn = None
+            return
+
+        def cb(_user, ptr, per, rk, nr):
+            try:
+                segs = np.ctypeslib.as_array(ptr, shape=(nr * per,)).reshape(nr, per)
+                gather(segs)
+                return 0
+            except BaseException as e:  # noqa: BLE001  (re-raised by run_episode)
+                self._xerr = e
+                return 1
+
+        fn = _lib.EXCHANGE_FN(cb)
+        self._chk(self.L.p2pmg_dqn_set_exchange(self._ctx, fn, None, int(rank), int(world)), "dqn_set_exchange")
+        self._xfn = fn
+
     # ----------------------------------------------------------------- replay memory
     def set_samples(self, samples):
         """Replay-mode sample indices: deque indices (0 = oldest) of random.sample(buffer, 32)
@@ -132,7 +166,11 @@ class DeviceDQNBatch(DeviceCommunityBatch):
             mask |= _lib.REC[r]
         args = _lib.EpisodeArgs(MODES[mode], _lib.RNG_REPLAY if rng == "replay" else _lib.RNG_PHILOX,
                                 int(episode), mask, float(epsilon), 0, 0)
-        self._chk(self.L.p2pmg_run_episode(self._ctx, C.byref(args)), "run_episode")
+        self._xerr = None
+        st = self.L.p2pmg_run_episode(self._ctx, C.byref(args))
+        if st != _lib.P2PMG_OK and self._xerr is not None:
+            raise _lib.P2PMGError(f"run_episode: the gradient exchange raised {self._xerr!r}") from self._xerr
+        self._chk(st, "run_episode")
         self._recorded = mask
 
     # ----------------------------------------------------------------- object-API primitives

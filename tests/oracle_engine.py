@@ -71,3 +71,38 @@ class OracleEngine:
     def get_q(self, first=0, count=None):
         q = self.ob.q
         return q[first:first + (len(q) - first if count is None else count)].copy()
+
+
+class OracleDQNEngine(OracleEngine):
+    """DeviceDQNBatch's interface (one shared network) computed by oracle/dqn.py, with the same
+    gradient layout (grad_segments, agents_per_block) and host exchange hook."""
+
+    def __init__(self, sh, S, N, R, T, q_dtype, device, seed, shared_q=True, learner="dqn", grad_segments=1,
+                 agents_per_block=0):
+        super().__init__(sh, S, N, R, T, q_dtype, device, seed, shared_q=True)
+        self.grad_segments, self.agents_per_block = grad_segments, agents_per_block
+        self._xchg = (None, 0, 1)
+
+    def _ensure(self):
+        if self.ob is None:
+            from oracle import dqn as odqn
+            gather, rank, world = self._xchg
+            self.ob = odqn.OracleDQNBatch(S=self.S, N=self.N, R=self.R, load_w=self._prof[0], pv_w=self._prof[1],
+                                          max_in=self._mi, env_time=self._env[0], env_tout=self._env[1],
+                                          theta0=odqn.glorot_init(1, 0), shared=True,
+                                          agents_per_block=self.agents_per_block, grad_segments=self.grad_segments,
+                                          rank=rank, world=world, exchange=gather)
+        return self.ob
+
+    def set_grad_exchange(self, gather, rank, world):
+        self._xchg = (gather, rank, world)
+        if self.ob is not None:
+            self.ob.exchange, self.ob.rank, self.ob.world = gather, rank, world
+
+    def run_episode(self, mode="train", rng="philox", episode=0, epsilon=1.0, record=(), philox="auto"):
+        self.last = self._ensure().run_episode(mode, rng="philox", seed=self.seed, episode=episode, eps=epsilon,
+                                               agent_ids=self.gids)
+
+    def get_weights(self, which="online", first=0, count=None):
+        arr = {"online": self.ob.theta, "target": self.ob.target, "adam_m": self.ob.m, "adam_v": self.ob.v}[which]
+        return arr.copy()

@@ -81,6 +81,63 @@ def test_two_rank_shared_table_exchange_is_world_size_invariant():
     assert np.allclose(means1, means2, rtol=0, atol=1e-9)
 
 
+def _dqn_worker(rank, world, port, q, kw):
+    import torch.distributed as dist
+    from oracle_engine import OracleDQNEngine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = ShardedTrainer(DQN_S, N, R, DQN_T, rank=rank, world=world, engine_factory=OracleDQNEngine, learner="dqn",
+                        exchange="host", **kw)
+    means = [tr.train_episode(0.9 ** (1 + e)) for e in range(2)]
+    per = tr.episode_rewards_global()
+    q.put((rank, means, per, tr.eng.get_weights("online"), tr.eng.get_weights("adam_v")))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+DQN_S, DQN_T = 4, 36
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_dqn_gradient_exchange_is_world_size_invariant():
+    """Config 5 on CPU: one shared DQN network, the gradient segments of both ranks gathered over
+    gloo every env step (host exchange) -> the weights, Adam state and every scenario's rewards equal
+    the single-process run with the same TOTAL segment count and block size, bit for bit."""
+    from oracle_engine import OracleDQNEngine
+    kw = dict(grad_segments=2, agents_per_block=3)
+    single = ShardedTrainer(DQN_S, N, R, DQN_T, engine_factory=OracleDQNEngine, learner="dqn", **kw)
+    means1 = [single.train_episode(0.9 ** (1 + e)) for e in range(2)]
+    per1 = single.episode_rewards_global()
+    w1, v1 = single.eng.get_weights("online"), single.eng.get_weights("adam_v")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dqn_worker, args=(r, 2, port, q, kw)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=240) for _ in range(2)], key=lambda g: g[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, means2, per2, w2, v2 in got:
+        assert np.array_equal(w1, w2) and np.array_equal(v1, v2), f"rank {rank} weights differ"
+        assert np.array_equal(per1, per2)
+        assert np.allclose(means1, means2, rtol=0, atol=1e-9)
+    from oracle.dqn import glorot_init
+    assert not np.array_equal(w1, glorot_init(1, 0))  # the network did train
+    # a different segment count changes the summation order (and so, in general, the bits)
+    other = ShardedTrainer(DQN_S, N, R, DQN_T, engine_factory=OracleDQNEngine, learner="dqn", grad_segments=1,
+                           agents_per_block=3)
+    [other.train_episode(0.9 ** (1 + e)) for e in range(2)]
+    assert np.allclose(other.eng.get_weights("online"), w1, rtol=1e-5, atol=1e-7)
+
+
+def test_dqn_trainer_rejects_bad_segments():
+    from oracle_engine import OracleDQNEngine
+    with pytest.raises(ValueError):
+        ShardedTrainer(DQN_S, N, R, DQN_T, engine_factory=OracleDQNEngine, learner="dqn", grad_segments=3)
+
+
 @pytest.mark.timeout(300)
 def test_bench_gpus_2_spawns_two_ranks():
     """``bench.py --gpus 2`` without torchrun starts 2 rank processes itself (gloo rendezvous on

@@ -100,6 +100,57 @@ def test_shared_table_two_ranks_match_single_context():
     assert np.allclose(means1, means2, rtol=0, atol=1e-9)
 
 
+DQN_KW = dict(learner="dqn", grad_segments=2, agents_per_block=8)
+DQN_S = 64
+
+
+def _dqn_episodes(tr):
+    return [tr.train_episode(0.9 ** (1 + e)) for e in range(EPISODES)]
+
+
+def _dqn_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = ShardedTrainer(DQN_S, N, R, T, rank=rank, world=world, device=0, exchange="host", **DQN_KW)
+    means = _dqn_episodes(tr)
+    per = tr.episode_rewards_global()
+    q.put((rank, means, per, tr.eng.get_weights("online"), tr.eng.get_weights("target"),
+           tr.eng.get_weights("adam_v"), tr.eng.grad_layout()))
+    dist.barrier()
+    tr.eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dqn_shared_network_two_ranks_match_single_context():
+    """Config 5 on the device: one shared Q-network, two ranks (two contexts on one GPU) gathering
+    their gradient segments over the process group every env step reproduce the single context with
+    the same total segment count and block size bit for bit: weights, target, Adam state and every
+    scenario's episode reward."""
+    single = ShardedTrainer(DQN_S, N, R, T, device=0, **DQN_KW)
+    assert single.eng.grad_layout() == {"segments": 2, "agents_per_block": 8, "blocks": 16}
+    means1 = _dqn_episodes(single)
+    per1 = single.episode_rewards_global()
+    w1, t1, v1 = (single.eng.get_weights(k) for k in ("online", "target", "adam_v"))
+    single.eng.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dqn_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=500) for _ in range(2)], key=lambda g: g[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, means2, per2, w2, t2, v2, layout in got:
+        assert layout == {"segments": 1, "agents_per_block": 8, "blocks": 8}
+        assert np.array_equal(w1, w2) and np.array_equal(t1, t2) and np.array_equal(v1, v2), f"rank {rank}"
+        assert np.array_equal(per1, per2)
+        assert np.allclose(means1, means2, rtol=0, atol=1e-9)
+
+
 def test_rccl_metrics_and_table_hash_world1():
     """The RCCL pieces on one rank: a world-1 communicator, the metric all-reduce (= the local
     sum of the episode rewards) and the table fingerprint all-gather (changes when the table does)."""
@@ -124,6 +175,17 @@ def _rccl_worker(rank, world, port, q, shared):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if shared == "dqn":
+        tr = ShardedTrainer(DQN_S, N, R, T, rank=rank, world=world, device=rank, exchange="rccl", **DQN_KW)
+        assert tr.eng.comm_nranks() == world
+        means = _dqn_episodes(tr)
+        per = tr.episode_rewards_global()
+        if rank == 0:
+            q.put((means, per, tr.eng.get_weights("online")))
+        dist.barrier()
+        tr.eng.close()
+        dist.destroy_process_group()
+        return
     kw = dict(shared_q=True, battery=dict(capacity=4.0e6 * 3600)) if shared else {}
     tr = ShardedTrainer(301, 4 if shared else 2, 1, 96, rank=rank, world=world, device=rank, exchange="rccl", **kw)
     assert tr.eng.comm_nranks() == world
@@ -138,18 +200,25 @@ def _rccl_worker(rank, world, port, q, shared):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("shared", [False, True])
+@pytest.mark.parametrize("shared", [False, True, "dqn"])
 def test_two_ranks_over_rccl_match_single_context(shared):
-    """Two ranks on two GPUs with the deltas and metrics exchanged over RCCL (xGMI) reproduce the
-    single-context run; the shared table's replicas agree bit for bit (fingerprint all-gather)."""
+    """Two ranks on two GPUs with the deltas / gradient segments and metrics exchanged over RCCL
+    (xGMI) reproduce the single-context run; the shared table's replicas agree bit for bit
+    (fingerprint all-gather), the shared DQN network's weights equal the single context's."""
     from p2pmicrogrid_amd import _lib
     if _lib.device_count() < 2:
         pytest.skip("needs 2 visible GPUs (the driver's 8-GPU node runs this path through bench.py)")
-    kw = dict(shared_q=True, battery=dict(capacity=4.0e6 * 3600)) if shared else {}
-    single = ShardedTrainer(301, 4 if shared else 2, 1, 96, device=0, **kw)
-    means1 = [single.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
-    per1 = single.episode_rewards_global()
-    q1 = single.eng.get_q(0, 1) if shared else None
+    if shared == "dqn":
+        single = ShardedTrainer(DQN_S, N, R, T, device=0, **DQN_KW)
+        means1 = _dqn_episodes(single)
+        per1 = single.episode_rewards_global()
+        q1 = single.eng.get_weights("online")
+    else:
+        kw = dict(shared_q=True, battery=dict(capacity=4.0e6 * 3600)) if shared else {}
+        single = ShardedTrainer(301, 4 if shared else 2, 1, 96, device=0, **kw)
+        means1 = [single.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+        per1 = single.episode_rewards_global()
+        q1 = single.eng.get_q(0, 1) if shared else None
     single.eng.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -163,6 +232,8 @@ def test_two_ranks_over_rccl_match_single_context(shared):
         assert p.exitcode == 0
     assert np.array_equal(per1, per2)
     assert np.allclose(means1, means2, rtol=0, atol=1e-9)
-    if shared:
+    if shared == "dqn":
+        assert np.array_equal(q1, extra)
+    elif shared:
         q2, hashes = extra
         assert np.array_equal(q1, q2) and hashes.shape == (2,) and hashes[0] == hashes[1]
