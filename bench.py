@@ -91,10 +91,12 @@ def epsilon_at(episode: int, eps0: float = 0.81, decay: float = 0.9, every: int 
     return eps
 
 
-def dist_setup(gpus: int):
+def dist_setup(gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if gpus is None:  # torchrun without --gpus: one rank per GPU of the launch
+        gpus = world
     if world != gpus:
         raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: launch N ranks with torchrun "
                          f"--nproc-per-node N, or run bench.py --gpus N without WORLD_SIZE (it spawns them)")
@@ -115,17 +117,24 @@ def _free_port() -> int:
 
 
 def visible_gpus() -> int:
-    """GPUs this node exposes, counted without initialising HIP in this process: the launcher
-    must stay GPU-free, because its children are the ranks (torch.cuda.device_count() does not
-    initialise the runtime on this image; HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES are honoured
-    by it)."""
+    """GPUs this node exposes, counted without any GPU runtime in this process (the launcher must
+    stay GPU-free: its children are the ranks).  The KFD topology lists one node per CPU socket and
+    GPU; GPU nodes carry a non-zero gpu_id.  A *_VISIBLE_DEVICES list narrows the count as the HIP
+    runtime would."""
     if os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
         return 0
-    try:
-        import torch
-        return int(torch.cuda.device_count())
-    except Exception:  # noqa: BLE001
-        return 0
+    import glob
+    n = 0
+    for path in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+        try:
+            n += int(open(path).read().strip() or 0) != 0
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
 
 
 def launch_ranks(argv, gpus: int) -> int:
@@ -135,16 +144,25 @@ def launch_ranks(argv, gpus: int) -> int:
     touches the GPU and never re-execs: the ranks are fresh child processes.  With fewer visible
     GPUs than ranks (a one-GPU rehearsal) ranks share devices round-robin and the line says so."""
     import subprocess
+    import tempfile
     n_dev = visible_gpus()
+    if n_dev == 0 and not os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
+        print("bench.py launcher: no GPU found in the KFD topology (/sys/class/kfd) for the ranks",
+              file=sys.stderr, flush=True)
+        return 2
     port = _free_port()
     procs = []
+    # rank 0's stdout goes to a file, read after the ranks exit: a pipe nobody reads while they run
+    # would block rank 0 once it filled (verbose libraries), and the others in its collectives
+    out_file = tempfile.TemporaryFile(mode="w+")
     for r in range(gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         if 0 < n_dev < gpus:
             env["P2PMG_BENCH_DEVICE"] = str(r % n_dev)
+            env["P2PMG_BENCH_RANKS_SHARE_GPU"] = "1"
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+                                      stdout=out_file if r == 0 else subprocess.DEVNULL, text=True))
     # wait for every rank; if one fails, stop the others (they would wait in a collective forever)
     import time as _t
     while any(p.poll() is None for p in procs):
@@ -154,8 +172,10 @@ def launch_ranks(argv, gpus: int) -> int:
                     p.kill()
             break
         _t.sleep(0.2)
-    out0, _ = procs[0].communicate()
     rcs = [p.wait() for p in procs]
+    out_file.seek(0)
+    out0 = out_file.read()
+    out_file.close()
     line = None
     for ln in (out0 or "").splitlines():
         ln = ln.strip()
@@ -188,6 +208,23 @@ def engine_class():
     return getattr(importlib.import_module(mod), cls)
 
 
+def dqn_engine_class():
+    """DeviceDQNBatch, or the CPU test suite's stand-in (P2PMG_BENCH_TEST_DQN_ENGINE=module:Class)."""
+    spec = os.environ.get("P2PMG_BENCH_TEST_DQN_ENGINE")
+    if not spec:
+        from p2pmicrogrid_amd.dqn import DeviceDQNBatch
+        return DeviceDQNBatch
+    import importlib
+    mod, cls = spec.split(":")
+    return getattr(importlib.import_module(mod), cls)
+
+
+def weights_fingerprint(w) -> int:
+    """64-bit fingerprint of an array's bits (host side; the shared network is 18 KB)."""
+    import hashlib
+    return int.from_bytes(hashlib.blake2b(np.ascontiguousarray(w).tobytes(), digest_size=8).digest(), "little")
+
+
 def all_gather_float(x: float, world: int):
     if world == 1:
         return [x]
@@ -202,6 +239,17 @@ def barrier(world):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+
+
+def exchange_kind(args, world: int) -> str:
+    """How the shared-state workloads sum their data-path state over the ranks: "rccl" (device
+    collectives over xGMI, the production path and the default) or "host" (gloo over the host,
+    a labelled rehearsal for ranks that share one GPU, where RCCL refuses a second rank)."""
+    if world == 1:
+        return "none"
+    if args.exchange != "auto":
+        return args.exchange
+    return "host" if os.environ.get("P2PMG_BENCH_RANKS_SHARE_GPU") else "rccl"
 
 
 def rccl_comm(eng, rank: int, world: int, required: bool = False) -> str:
@@ -258,13 +306,14 @@ MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_16x
 DQN_FWD_FLOP = 2 * (5 * 64 + 64 * 64 + 64 * 1)  # QNetwork (rl.py:135-148): 8,960 FLOP per row
 
 
-def collective_record(eng, world: int, steps: int):
-    """The data-path all-reduces of the timed episodes (shared-table delta once per episode, DQN
-    gradient once per env step): HIP-event time on the rank's stream, rank 0's view (world > 1)."""
+def collective_record(eng, world: int, steps: int, kind: str = "RCCL allReduce (data path)"):
+    """The data-path collectives of the timed episodes (shared-table delta all-reduce once per
+    episode, DQN gradient-segment all-gather once per env step): HIP-event time on the rank's
+    stream, every call counted, rank 0's view (world > 1)."""
     if world <= 1 or not hasattr(eng, "collective_ms"):
         return None
     total, n = eng.collective_ms()
-    return {"kind": "RCCL allReduce (data path)", "calls": n, "ms_total": total,
+    return {"kind": kind, "calls": n, "ms_total": total,
             "ms_per_step": total / max(steps, 1), "us_per_call": 1e3 * total / n if n else None}
 
 
@@ -304,16 +353,21 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     train launch (32-sample batches on f32 MFMA) + gradient reduce (+ RCCL all-reduce over ranks)
     + Adam/soft update.  One bench step = one training episode (T env steps) of every scenario."""
     from p2pmicrogrid_amd.dataset import scenario_batch
-    from p2pmicrogrid_amd.dqn import DeviceDQNBatch
     first = rank * S
     inp = scenario_batch(S, N, T, first_scenario=first)
-    eng = DeviceDQNBatch(S, N, R, T, shared=True, device=local, scenario_offset=first, init_seed=0)
+    eng = dqn_engine_class()(S, N, R, T, shared=True, device=local, scenario_offset=first, init_seed=0)
     eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
     eng.set_profiles(inp.load_w, inp.pv_w)
     eng.set_max_in(inp.max_in)
     eng.set_temperatures(inp.t_in0, inp.t_m0)
     del inp
-    comm_err = rccl_comm(eng, rank, world, required=True)  # gradient all-reduce every env step + metrics
+    xk = exchange_kind(args, world)
+    if xk == "host":  # rehearsal: the gradient segments gathered over gloo every env step
+        from p2pmicrogrid_amd.distributed import all_gather_rows
+        eng.set_grad_exchange(lambda rows: all_gather_rows(rows, rank, world), rank, world)
+        comm_err = "host-rehearsal exchange (no RCCL communicator)"
+    else:  # gradient-segment all-gather every env step + metrics over RCCL
+        comm_err = rccl_comm(eng, rank, world, required=True)
     record = ("reward", "cost")
     eng.run_episode("fill", "philox", episode=0, epsilon=1.0, record=record)  # community.init_buffers
     eng.reset_temperatures_philox(1, 0.3)
@@ -339,7 +393,10 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     rank_times = all_gather_float(time.perf_counter() - t0, world)
     dt = max(rank_times)
     kms = eng.kernel_times()
-    coll = collective_record(eng, world, args.steps)
+    coll = collective_record(eng, world, args.steps, "RCCL allGather of the gradient segments (data path)")
+    # every rank's replica of the shared network (the same Adam step on the same gathered sum)
+    from p2pmicrogrid_amd.distributed import all_gather_concat
+    fps = all_gather_concat(np.array([weights_fingerprint(eng.get_weights("online"))], np.uint64), world)
     steps_per_episode = S * N * T
     flop = dqn_flop_per_agent_step(R)
     episode_ms = float(np.mean(kms)) if len(kms) else float("nan")
@@ -364,8 +421,13 @@ def main_dqn(args, rank, world, local, S, N, R, T):
             "mean_episode_reward": metrics[0] / metrics[1],
             "rccl_nranks": eng.comm_nranks() if not comm_err else 0,
             "rank_times_s": rank_times,
+            "grad_layout": eng.grad_layout(),
+            "network_replicas_identical": bool(np.all(fps == fps[0])),
         }
-        if coll:
+        assert out["network_replicas_identical"], f"shared-network replicas differ across ranks: {fps}"
+        if world > 1:
+            out["exchange"] = "host-rehearsal" if xk == "host" else "rccl"
+        if coll and xk != "host":
             out["collective"] = coll
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_dqn(args.cpu_seconds, R=R, T=T)
@@ -515,7 +577,8 @@ def load_traffic(path: str, workload: str):
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = ranks (default 1; under torchrun the launch's WORLD_SIZE)")
     ap.add_argument("--steps", type=int, default=50, help="timed episodes")
     ap.add_argument("--warmup", type=int, default=5, help="untimed episodes")
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS),
@@ -530,15 +593,21 @@ def main():
     ap.add_argument("--metric-every", type=int, default=50,
                     help="episodes between RCCL all-reduces of the episode metrics (community.py:279)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "rccl", "host"],
+                    help="data-path exchange over ranks: rccl (xGMI, default when every rank has its own GPU) or "
+                         "host (gloo rehearsal; auto picks it only when the launcher maps ranks onto shared GPUs)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary for roofline.traffic (default profiles/pmc_traffic[_<workload>].json)")
     args = ap.parse_args()
-    if args.gpus < 1:
+    if args.gpus is not None and args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        return launch_ranks(sys.argv[1:], args.gpus)
+    if "WORLD_SIZE" not in os.environ:
+        args.gpus = args.gpus or 1
+        if args.gpus > 1:
+            return launch_ranks(sys.argv[1:], args.gpus)
 
     rank, world, local = dist_setup(args.gpus)
+    args.gpus = world
     from p2pmicrogrid_amd.dataset import apply_asset_mix, asset_mix, scenario_batch
     DeviceCommunityBatch = engine_class()
 
@@ -569,14 +638,21 @@ def main():
     elif battery:
         eng.set_battery(BATTERY_J)
     # episode metrics (+ the shared table's per-episode delta all-reduce, which needs RCCL)
-    comm_err = rccl_comm(eng, rank, world, required=shared)
+    xk = exchange_kind(args, world)
+    if xk == "host":  # rehearsal: int64 deltas and metrics summed over gloo
+        comm_err = "host-rehearsal exchange (no RCCL communicator)"
+    else:
+        comm_err = rccl_comm(eng, rank, world, required=shared)
     record = ("reward", "cost")
 
     def episode(e):
         if shared:
             eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record,
                             next_epsilon=epsilon_at(e + 1))
-            if world > 1:
+            if world > 1 and xk == "host":
+                from p2pmicrogrid_amd.distributed import all_reduce_int64
+                eng.set_q_delta(all_reduce_int64(eng.get_q_delta(), world))
+            elif world > 1:
                 eng.allreduce_q_delta()
             eng.apply_q_delta()
             eng.reset_temperatures_philox(e + 1, 0.3)  # agent.reset() at the end of train_episode
@@ -607,7 +683,11 @@ def main():
     coll = collective_record(eng, world, args.steps)
     ep_reward = metrics[0] / metrics[1]
     nranks = eng.comm_nranks() if not comm_err else 0
-    hashes = eng.table_hash_allgather() if shared else None  # every replica of the shared table
+    if shared and xk == "host":  # every replica's fingerprint, gathered over gloo
+        from p2pmicrogrid_amd.distributed import all_gather_concat
+        hashes = all_gather_concat(eng.table_hash_allgather().astype(np.uint64), world)
+    else:
+        hashes = eng.table_hash_allgather() if shared else None  # every replica of the shared table
 
     steps_per_episode = S * N * T
     value = world * steps_per_episode * args.steps / dt
@@ -665,7 +745,9 @@ def main():
             out["test_engine"] = os.environ["P2PMG_BENCH_TEST_ENGINE"]
         if comm_err:
             out["rccl_error"] = comm_err
-        if coll:
+        if world > 1:
+            out["exchange"] = "host-rehearsal" if xk == "host" else "rccl"
+        if coll and xk != "host":
             out["collective"] = coll
         if shared:
             out["table_replicas_identical"] = bool(np.all(hashes == hashes[0]))

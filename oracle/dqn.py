@@ -135,6 +135,206 @@ def gradients(theta, s, a, r, ns, target, gamma: float, clip: float = 1.0):
     return g.astype(F32), loss.astype(F32)
 
 
+# ----------------------------------------------------------------------------- device order
+# The same arithmetic in the summation order of the HIP kernels (p2pmg_dqn.hip), so the device
+# can be held to it bit for bit.  The f32 MFMA is exactly a k-ordered fmaf chain (MI355X guide,
+# FP32-input MFMA numerics), DPP / permlane sums are the pairwise trees spelled out below, and
+# every other op rounds on its own (-ffp-contract=off).  forward()/gradients() above (NumPy
+# matmul order) stay as the independent second check, within the north_star tolerance.
+
+def fmaf(a, b, c):
+    """float32 fused multiply-add with ONE rounding: a * b is exact in float64 (24 + 24 bits);
+    the float64 sum is taken with round-to-odd (TwoSum error folded into the last bit), which
+    rounds correctly to float32 afterwards (53 >= 24 + 2 bits)."""
+    a, b, c = (np.asarray(x, F32) for x in (a, b, c))
+    p = a.astype(np.float64) * b.astype(np.float64)
+    cc = c.astype(np.float64)
+    with np.errstate(invalid="ignore", over="ignore"):
+        sm = p + cc
+        bb = sm - p
+        err = (p - (sm - bb)) + (cc - bb)
+        odd = np.frombuffer(np.ascontiguousarray(sm, np.float64).tobytes(), np.int64).reshape(sm.shape) & 1
+        fix = (err != 0) & (odd == 0) & np.isfinite(sm)
+        sm = np.where(fix, np.nextafter(sm, np.where(err > 0, np.inf, -np.inf)), sm)
+    return sm.astype(F32)
+
+
+def tree_sum(v, axis=-1):
+    """Pairwise tree of adjacent elements (v0 + v1) + (v2 + v3) ... over a power-of-two axis: the
+    DPP quad_perm / row_half_mirror / row_mirror + permlane16 / permlane32 swap sums (x + swap(x)
+    adds the same two operands in both lanes)."""
+    v = np.moveaxis(np.asarray(v, F32), axis, -1)
+    while v.shape[-1] > 1:
+        v = (v[..., 0::2] + v[..., 1::2]).astype(F32)
+    return v[..., 0]
+
+
+def relu32(x):
+    x = np.asarray(x, F32)
+    return np.where(x > 0, x, F32(0)).astype(F32)
+
+
+def act_q(theta, obs):
+    """Greedy Q values of dqn_act_kernel / dqn_act_shared_kernel (ActorModel.greedy_action
+    rl.py:188-196): layer 1 as p2p * W1[3], then fmaf with bal, tnorm, time (features 3, 2, 1, 0),
+    the action term added per action value; layer 2 as an fmaf chain over k = 0..63 from +0;
+    layer 3 as the pairwise tree over the 64 units (wave_sum), then + b3.
+    theta [4609]; obs [..., 4] -> q [..., 3]."""
+    p = unpack(theta)
+    obs = np.asarray(obs, F32)
+    W1, b1, W2, b2, w3, b3 = p["W1"], p["b1"], p["W2"], p["b2"], p["W3"][:, 0], p["b3"][0]
+    o = obs[..., None, :]
+    z = (o[..., 3] * W1[3]).astype(F32)
+    z = fmaf(o[..., 2], W1[2], z)
+    z = fmaf(o[..., 1], W1[1], z)
+    z = fmaf(o[..., 0], W1[0], z)
+    hs = [relu32(z + b1), relu32(fmaf(F32(0.5), W1[4], z) + b1), relu32((z + W1[4]).astype(F32) + b1)]
+    out = []
+    for h in hs:
+        acc = np.zeros(h.shape, F32)
+        for k in range(H):
+            acc = fmaf(h[..., k:k + 1], W2[k], acc)
+        out.append(tree_sum((relu32(acc + b2) * w3).astype(F32)) + b3)
+    return np.stack(out, -1).astype(F32)
+
+
+def api_forward(theta, x):
+    """dqn_forward_kernel (QNetwork.call on explicit rows, rl.py:147-148): layer 1 as an fmaf
+    chain over the 5 inputs, layer 2 over k = 0..63, layer 3 as an fmaf chain over the units,
+    + b3.  theta [4609]; x [..., 5] -> q [...]."""
+    p = unpack(theta)
+    x = np.asarray(x, F32)
+    z = np.zeros(x.shape[:-1] + (H,), F32)
+    for k in range(N_IN):
+        z = fmaf(x[..., k:k + 1], p["W1"][k], z)
+    h1 = relu32(z + p["b1"])
+    acc = np.zeros(h1.shape, F32)
+    for k in range(H):
+        acc = fmaf(h1[..., k:k + 1], p["W2"][k], acc)
+    h2 = relu32(acc + p["b2"])
+    out = np.zeros(x.shape[:-1], F32)
+    for j in range(H):
+        out = fmaf(h2[..., j], p["W3"][j, 0], out)
+    return (out + p["b3"][0]).astype(F32)
+
+
+def _chain_k(h, W2):
+    """fmaf chain over k = 0..63 from +0: h [..., rows, 64] x W2 [..., 64, 64] (rows of W2 = k)."""
+    acc = np.zeros(h.shape[:-1] + (W2.shape[-1],), F32)
+    for k in range(W2.shape[-2]):
+        acc = fmaf(h[..., k:k + 1], W2[..., None, k, :], acc)
+    return acc
+
+
+def _train_layer23(h1, W2, b2, w3):
+    """dqn_train_kernel layers 2-3 of one network: Z2^T = W2^T H1^T on MFMA (fmaf chain over
+    k = 0..63), ReLU, then each wave's 16 units as the pairwise tree (in-lane pairs, reduce4_groups)
+    and the 4 waves added in wave order (qpart), + b3 by the caller.  Returns (z2 pre-ReLU, q sum).
+    h1 [..., 32, 64]; W2 [..., 64, 64]; b2, w3 [..., 64]."""
+    pre = (_chain_k(h1, W2) + b2[..., None, :]).astype(F32)
+    v = (relu32(pre) * w3[..., None, :]).astype(F32)
+    q = tree_sum(v[..., 0:16])
+    for w in range(1, 4):
+        q = (q + tree_sum(v[..., 16 * w:16 * w + 16])).astype(F32)
+    return pre, q
+
+
+def train_block(theta, target, batches, gamma: float, counts=None):
+    """dqn_train_kernel workgroups (Trainer._train rl.py:307-333 up to the optimizer), in the
+    kernel's order, for nb blocks at once.  theta / target [4609] (a shared network) or [nb, 4609]
+    (one network per block); batches [nb, n_ag, 32, 10] (s[4], a, r, ns[4]) or [n_ag, 32, 10] (one
+    block); counts [nb]: agents of each block (default n_ag; a shorter block's trailing slots are
+    ignored).  The gradient accumulators run ACROSS a block's agents as the kernel's registers do:
+    dW2 as the MFMA chain over (agent, q = 0..7, b = 8 k + q); dW1 / db1 per row group g4 over
+    (agent, r, rt) rows b = 16 rt + 4 g4 + r, then the 4 groups pairwise; dW3 / db2 per data-row
+    lane c over (agent, rt) rows b = 16 rt + c, then the 16 lanes pairwise; db3 per agent pairwise
+    over the lanes of dq[c] + dq[16 + c], chained over agents.
+    Returns (gradient partials [nb, 4609] f32 (W1 not clipped), loss [nb, n_ag]); without a block
+    axis in `batches`, ([4609], [n_ag])."""
+    bt = np.asarray(batches, F32)
+    single = bt.ndim == 3
+    if single:
+        bt = bt[None]
+    nb, n_ag = bt.shape[0], bt.shape[1]
+    cnt = np.full(nb, n_ag) if counts is None else np.asarray(counts)
+    P, T = unpack(theta), unpack(target)
+    if np.ndim(theta) == 1:  # one shared network: a block axis of length 1 broadcasts
+        P = {k: v[None] for k, v in P.items()}
+        T = {k: v[None] for k, v in T.items()}
+    gW2 = np.zeros((nb, H, H), F32)
+    gx1 = np.zeros((nb, 4, N_IN, H), F32)      # [block][row group g4][input k][unit]
+    gb1 = np.zeros((nb, 4, H), F32)
+    gW3 = np.zeros((nb, 16, H), F32)           # [block][lane c][unit]
+    gb2 = np.zeros((nb, 16, H), F32)
+    gb3 = np.zeros(nb, F32)
+    losses = np.zeros((nb, n_ag), F32)
+    b3t, b3o = T["b3"][:, 0], P["b3"][:, 0]
+    rows_g = [[16 * rt + 4 * np.arange(4) + rr for rt in range(2)] for rr in range(4)]
+    for ag in range(n_ag):
+        on = (ag < cnt)                          # blocks that still have an agent at this slot
+        x = bt[:, ag]                            # [nb, 32, 10]
+        s5, r, ns = x[..., 0:5], x[..., 5], x[..., 6:10]
+        # target network on (ns, a') for the 3 action values
+        z = np.zeros((nb, 32, H), F32)
+        for k in range(4):
+            z = fmaf(ns[..., k:k + 1], T["W1"][:, None, k, :], z)
+        qt = []
+        for av in ACTION_VALUES:
+            h1t = relu32(fmaf(av, T["W1"][:, None, 4, :], z) + T["b1"][:, None, :])
+            _, qs = _train_layer23(h1t, T["W2"], T["b2"], T["W3"][..., 0])
+            qt.append((qs + b3t[:, None]).astype(F32))
+        # online network on (s, a): features 0..3 then the action input (second MFMA)
+        z = np.zeros((nb, 32, H), F32)
+        for k in range(N_IN):
+            z = fmaf(s5[..., k:k + 1], P["W1"][:, None, k, :], z)
+        pre1 = (z + P["b1"][:, None, :]).astype(F32)
+        h1 = relu32(pre1)
+        pre2, qs = _train_layer23(h1, P["W2"], P["b2"], P["W3"][..., 0])
+        h2 = relu32(pre2)
+        q = (qs + b3o[:, None]).astype(F32)
+        y = (r + F32(gamma) * np.maximum(np.maximum(qt[0], qt[1]), qt[2])).astype(F32)
+        diff = (q - y).astype(F32)
+        dq = (F32(2.0 / 32) * diff).astype(F32)                       # [nb, 32]
+        sq = (diff * diff).astype(F32)
+        losses[:, ag] = tree_sum((sq[:, 0:16] + sq[:, 16:32]).astype(F32)) / F32(32)
+        gb3 = np.where(on, (gb3 + tree_sum((dq[:, 0:16] + dq[:, 16:32]).astype(F32))).astype(F32), gb3)
+        # backward: dZ2, dW3, db2 (lane c holds rows c and 16 + c)
+        w3o = P["W3"][..., 0][:, None, :]
+        dz2 = np.where(pre2 > 0, (dq[..., None] * w3o).astype(F32), F32(0)).astype(F32)
+        prod3 = (h2 * dq[..., None]).astype(F32)
+        m = on[:, None, None]
+        for rt in range(2):
+            gW3 = np.where(m, (gW3 + prod3[:, 16 * rt:16 * rt + 16]).astype(F32), gW3)
+            gb2 = np.where(m, (gb2 + dz2[:, 16 * rt:16 * rt + 16]).astype(F32), gb2)
+        # dW2 = H1^T dZ2, MFMA K order b = 8 k + q
+        for qq in range(8):
+            for k in range(4):
+                b = 8 * k + qq
+                gW2 = np.where(m, fmaf(h1[:, b, :, None], dz2[:, b, None, :], gW2), gW2)
+        # dH1 = dZ2 W2^T, K order j = 16 g + kk; dZ1 = dH1 [pre1 > 0]
+        dh1 = np.zeros((nb, 32, H), F32)
+        for kk in range(16):
+            for g in range(4):
+                j = 16 * g + kk
+                dh1 = fmaf(dz2[..., j:j + 1], P["W2"][:, None, :, j], dh1)
+        dz1 = np.where(pre1 > 0, dh1, F32(0)).astype(F32)
+        m4 = on[:, None, None, None]
+        for rr in range(4):
+            for rt in range(2):
+                rows = rows_g[rr][rt]                                   # one row per group g4
+                gb1 = np.where(m, (gb1 + dz1[:, rows]).astype(F32), gb1)
+                for k in range(N_IN):
+                    gx1[:, :, k] = np.where(m4[..., 0], fmaf(s5[:, rows, k][..., None], dz1[:, rows], gx1[:, :, k]),
+                                            gx1[:, :, k])
+    g1 = ((gx1[:, 0] + gx1[:, 1]).astype(F32) + (gx1[:, 2] + gx1[:, 3]).astype(F32)).astype(F32)
+    gb1s = ((gb1[:, 0] + gb1[:, 1]).astype(F32) + (gb1[:, 2] + gb1[:, 3]).astype(F32)).astype(F32)
+    g = np.concatenate([g1.reshape(nb, -1), gb1s, gW2.reshape(nb, -1), tree_sum(gb2, axis=1),
+                        tree_sum(gW3, axis=1), gb3[:, None]], axis=1).astype(F32)
+    if single:
+        return g[0], losses[0]
+    return g, losses
+
+
 def adam_lr(step: int, dp: DQNParams = DQNParams()) -> np.float32:
     """lr * sqrt(1 - beta2^t) / (1 - beta1^t), t = step (1-based), in float64 -> float32."""
     t = np.asarray(step, np.float64)
@@ -259,6 +459,9 @@ class OracleDQNBatch:
     rank: int = 0
     world: int = 1
     exchange: Optional[Callable] = None
+    # "device": the HIP kernels' summation order (act_q, train_block: bit-exact target);
+    # "matmul": NumPy matmul order (q_values, gradients: the independent second check)
+    order: str = "device"
 
     def __post_init__(self):
         self.T = self.load_w.shape[-1]
@@ -286,6 +489,36 @@ class OracleDQNBatch:
         else:
             self.buy, self.inj, self.p2p = (np.asarray(x, F32).reshape(-1, T) for x in self.price_table)
 
+    def _train_device(self, b, dp):
+        """The train launch(es) of one env step in the kernels' order: shared network = one
+        train_block per workgroup (block_layout), then the segment reduction + Adam; per-agent
+        networks = one train_block per agent with its own Adam step."""
+        A = b.shape[0]
+        if self.shared:
+            _, apb, bps, blocks = block_layout(A, self.grad_segments, self.agents_per_block)
+            bb = np.zeros((len(blocks), apb) + b.shape[1:], F32)
+            for k, (a0, n) in enumerate(blocks):
+                bb[k, :n] = b[a0:a0 + n]
+            counts = np.array([n for _, n in blocks])
+            partials, lb = train_block(self.theta[0], self.target[0], bb, dp.gamma, counts)
+            ls = np.concatenate([lb[k, :n] for k, (_, n) in enumerate(blocks)])
+            adam_step(self.theta, self.m, self.v, self._reduce_partials(partials, bps)[None], self.step, dp)
+            return ls
+        gr, ls = train_block(self.theta, self.target, b[:, None], dp.gamma)
+        adam_step(self.theta, self.m, self.v, gr, self.step, dp)
+        return ls[:, 0]
+
+    def _reduce_partials(self, partials, bps):
+        """fold_segments -> (exchange over ranks) -> sum_segments -> mean over all agents."""
+        segs = fold_segments(partials, bps)
+        A_local = self.S * self.N
+        if self.world > 1:
+            rows = np.zeros((self.world, segs.size), F32)
+            rows[self.rank] = segs.ravel()
+            self.exchange(rows)
+            segs = rows.reshape(-1, N_PARAMS)
+        return sum_segments(segs) * (F32(1) / F32(A_local * self.world))
+
     def _shared_gradient(self, gr):
         """Mean gradient of every agent of every rank in the device's summation structure: block
         partials (agents in order), each segment folded by fold_segments, every rank's segments
@@ -298,13 +531,7 @@ class OracleDQNBatch:
             for a in range(a0, a0 + n):
                 acc = acc + gr[a]
             partials[k] = acc
-        segs = fold_segments(partials, bps)
-        if self.world > 1:
-            rows = np.zeros((self.world, segs.size), F32)
-            rows[self.rank] = segs.ravel()
-            self.exchange(rows)
-            segs = rows.reshape(-1, N_PARAMS)
-        return sum_segments(segs) * (F32(1) / F32(A * self.world))
+        return self._reduce_partials(partials, bps)
 
     def _env(self, arr, t):
         return arr[:, t] if arr.shape[0] == self.S else np.broadcast_to(arr[0, t], (self.S,))
@@ -355,7 +582,12 @@ class OracleDQNBatch:
                 p2pf = (seq_sum(powers) / F32(N)) / mi                     # agent.py:203
                 obs = np.stack([np.broadcast_to(time_t[:, None], (S, N)), tnorm, bal, p2pf], -1).astype(F32)
                 th = self._nets(self.theta).reshape(A, N_PARAMS) if not self.shared else self.theta
-                if self.shared:
+                if self.order == "device":
+                    if self.shared:
+                        q = act_q(self.theta[0], obs.reshape(A, 4)).reshape(S, N, 3)
+                    else:
+                        q = np.stack([act_q(th[k], obs.reshape(A, 4)[k]) for k in range(A)]).reshape(S, N, 3)
+                elif self.shared:
                     q = q_values(self.theta[0], obs.reshape(A, 4)).reshape(S, N, 3)
                 else:
                     q = q_values(th, obs.reshape(A, 1, 4)).reshape(S, N, 3)
@@ -394,7 +626,9 @@ class OracleDQNBatch:
                 b = self.buf[np.arange(S)[:, None, None], np.arange(N)[None, :, None], self.slots(idx)]  # [S,N,k,10]
                 b = b.reshape(A, -1, 10)
                 self.step += 1
-                if self.shared:
+                if self.order == "device":
+                    ls = self._train_device(b, dp)
+                elif self.shared:
                     gr, ls = gradients(np.broadcast_to(self.theta[0], (A, N_PARAMS)), b[..., 0:4], b[..., 4],
                                        b[..., 5], b[..., 6:10], np.broadcast_to(self.target[0], (A, N_PARAMS)),
                                        dp.gamma, dp.clip)

@@ -14,6 +14,9 @@ class BenchOracleEngine(OracleEngine):
         if fail is not None and fail == os.environ.get("RANK"):
             raise RuntimeError("test: this rank fails at engine construction")
         super().__init__(Shard(0, 1, scenario_offset, S), S, N, R, T, q_dtype, device, seed, shared_q=shared_q)
+        noise = int(os.environ.get("P2PMG_BENCH_TEST_NOISE", "0"))  # a chatty rank (launcher pipe test)
+        for _ in range(noise // 1000):
+            print("x" * 999, flush=False)
         self.device = device
         self._times = []
 
@@ -51,3 +54,45 @@ class BenchOracleEngine(OracleEngine):
 
     def comm_nranks(self):
         return 1
+
+    def table_hash_allgather(self):
+        import hashlib
+        h = hashlib.blake2b(np.ascontiguousarray(self.ob.q).tobytes(), digest_size=8).digest()
+        return np.array([int.from_bytes(h, "little")], np.uint64)
+
+
+class BenchOracleDQNEngine:
+    """The DeviceDQNBatch calls main_dqn makes, on oracle/dqn.py (one shared network)."""
+
+    def __init__(self, S, N, R, T, shared=True, device=0, scenario_offset=0, init_seed=0, seed=42):
+        from oracle_engine import OracleDQNEngine
+        self._e = OracleDQNEngine(Shard(0, 1, scenario_offset, S), S, N, R, T, "f32", device, seed)
+        self.S, self.N, self.R, self.T = S, N, R, T
+
+    def __getattr__(self, name):  # set_env, set_profiles, ..., run_episode, episode_reward, get_weights
+        return getattr(self._e, name)
+
+    def comm_init(self, uid, rank, world):
+        raise RuntimeError("no RCCL in the CPU test engine")
+
+    def sync(self):
+        pass
+
+    def reset_kernel_times(self):
+        pass
+
+    def kernel_times(self):
+        return np.array([], np.float64)
+
+    def close(self):
+        pass
+
+    def allreduce_metrics(self):
+        r = self.episode_reward().astype(np.float64)
+        return float(r.sum()), int(r.size)
+
+    def comm_nranks(self):
+        return 1
+
+    def grad_layout(self):
+        return {"segments": self._e.grad_segments, "agents_per_block": self._e.agents_per_block, "blocks": None}

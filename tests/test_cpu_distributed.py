@@ -172,6 +172,74 @@ def test_bench_gpus_2_spawns_two_ranks():
     assert d1["mean_episode_reward"] == pytest.approx(d["mean_episode_reward"], rel=1e-12)
 
 
+def _bench_env(**extra):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["P2PMG_BENCH_TEST_ENGINE"] = "bench_test_engine:BenchOracleEngine"
+    env["PYTHONPATH"] = os.pathsep.join([root, os.path.join(root, "tests"), env.get("PYTHONPATH", "")])
+    env.update(extra)
+    return root, env
+
+
+def _bench_line(root, env, *args):
+    import json
+    import subprocess
+    import sys
+    cmd = [sys.executable, os.path.join(root, "bench.py"), *args, "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    return lines[0]
+
+
+@pytest.mark.timeout(300)
+def test_bench_launcher_survives_chatty_rank0():
+    """Rank 0 writing more than 1 MB before its JSON line (a verbose library) must not block on a
+    full pipe: the launcher collects its output in a file and still returns the line."""
+    root, env = _bench_env(P2PMG_BENCH_TEST_NOISE=str(1_200_000))
+    d = _bench_line(root, env, "--gpus", "2", "--steps", "1", "--warmup", "0", "--scenarios", "2", "--horizon", "8")
+    assert d["n_gpus"] == 2 and d["launcher"]["rank_exit_codes"] == [0, 0]
+
+
+@pytest.mark.timeout(300)
+def test_bench_host_rehearsal_shared_table():
+    """configs[2]'s exchange step at --gpus 2 with --exchange host (the one-GPU rehearsal): int64
+    deltas summed over gloo, every replica's table fingerprint equal, and the same mean reward as
+    one rank with both shards (integer sums do not depend on the split)."""
+    root, env = _bench_env()
+    common = ["--workload", "config3", "--agents", "4", "--horizon", "12", "--steps", "2", "--warmup", "1"]
+    d = _bench_line(root, env, "--gpus", "2", "--exchange", "host", "--scenarios", "3", *common)
+    assert d["exchange"] == "host-rehearsal" and d["table_replicas_identical"] and d["n_gpus"] == 2
+    d1 = _bench_line(root, env, "--scenarios", "6", *common)
+    assert d1["mean_episode_reward"] == pytest.approx(d["mean_episode_reward"], rel=1e-12)
+
+
+@pytest.mark.timeout(300)
+def test_bench_host_rehearsal_dqn():
+    """configs[4] at --gpus 2 with --exchange host: the gradient segments gathered over gloo every env
+    step; the shared network's replicas on both ranks are bit-identical."""
+    root, env = _bench_env(P2PMG_BENCH_TEST_DQN_ENGINE="bench_test_engine:BenchOracleDQNEngine")
+    d = _bench_line(root, env, "--gpus", "2", "--exchange", "host", "--workload", "config5", "--scenarios", "2",
+                    "--horizon", "40", "--steps", "1", "--warmup", "0")
+    assert d["exchange"] == "host-rehearsal" and d["network_replicas_identical"] and d["n_gpus"] == 2
+
+
+def test_visible_gpus_without_runtime(monkeypatch):
+    """The launcher counts GPUs from the KFD topology (no HIP / torch.cuda in the parent) and
+    honours a *_VISIBLE_DEVICES list."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.delenv("P2PMG_BENCH_TEST_ENGINE", raising=False)
+    n = bench.visible_gpus()
+    assert n >= 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert bench.visible_gpus() == min(n, 1)
+
+
 def test_bench_rejects_world_mismatch():
     import subprocess
     import sys
