@@ -324,14 +324,56 @@ def dqn_flop_per_agent_step(R: int) -> int:
     return 32 * 6 * DQN_FWD_FLOP + 3 * (R + 1) * DQN_FWD_FLOP
 
 
-def cpu_baseline_dqn(seconds: float, S: int = 2, N: int = 2, R: int = 1, T: int = 96):
+def _cpu_worker(job):
+    """One process of the all-cores CPU baseline: a bench.py CPU-baseline function by name."""
+    name, kw = job
+    return globals()[name](**kw)
+
+
+def cpu_workers() -> int:
+    """Host cores the CPU baseline may use: this process's CPU affinity, capped at 16 (a GPU box's
+    CPU share per GPU; os.cpu_count() there reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("P2PMG_CPU_WORKERS", "16"))))
+
+
+def cpu_baseline_all_cores(name: str, kw: dict, workers: int) -> dict:
+    """The same CPU-baseline function in `workers` concurrent single-threaded processes, each on its
+    own scenario slice (first_scenario = k * S), started together; value = the sum of their rates.
+    The one-core figure of the same run is kept under "one_core"."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    old = os.environ.get("OMP_NUM_THREADS")
+    os.environ["OMP_NUM_THREADS"] = "1"  # one thread per worker process (NumPy / BLAS)
+    try:
+        jobs = [(name, dict(kw, first=k * kw.get("S", 1))) for k in range(workers)]
+        with cf.ProcessPoolExecutor(workers, mp_context=mp.get_context("spawn")) as ex:
+            res = list(ex.map(_cpu_worker, jobs))
+    finally:
+        if old is None:
+            os.environ.pop("OMP_NUM_THREADS", None)
+        else:
+            os.environ["OMP_NUM_THREADS"] = old
+    out = dict(res[0])
+    out["one_core"] = {"value": res[0]["value"], "sample": res[0]["sample"]}
+    out.update(value=sum(r["value"] for r in res), cores=workers, workers=workers, threads_per_worker=1,
+               per_worker=[r["value"] for r in res],
+               sample=f"{workers} concurrent processes x ({res[0]['sample']})")
+    return out
+
+
+def cpu_baseline_dqn(seconds: float, S: int = 2, N: int = 2, R: int = 1, T: int = 96, first: int = 0):
     """oracle/dqn.py (NumPy, one thread) on a bounded sample: one fill episode, then train episodes."""
     from oracle import dqn as odqn
     from p2pmicrogrid_amd.dataset import scenario_batch
-    inp = scenario_batch(S, N, T)
+    inp = scenario_batch(S, N, T, first_scenario=first)
     th0 = odqn.glorot_init(1, 0)
     ob = odqn.OracleDQNBatch(S=S, N=N, R=R, load_w=inp.load_w, pv_w=inp.pv_w, max_in=inp.max_in,
-                             env_time=inp.time[None], env_tout=inp.t_out, theta0=th0, shared=True)
+                             env_time=inp.time[None], env_tout=inp.t_out, theta0=th0, shared=True,
+                             order="matmul")  # the vectorised NumPy form (the kernel-order form is a checker)
     ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
     ob.run_episode("fill", rng="philox", episode=0, eps=1.0)
     t0 = time.perf_counter()
@@ -343,6 +385,7 @@ def cpu_baseline_dqn(seconds: float, S: int = 2, N: int = 2, R: int = 1, T: int 
             break
     dt = time.perf_counter() - t0
     return {"value": S * N * T * done / dt, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "label": "CPU restatement (oracle/dqn.py, NumPy matmul order)",
             "sample": f"{S} scenarios x N={N} DQN agents (R={R}, T={T}, shared network), {done} training "
                       f"episodes after one fill episode, oracle/dqn.py NumPy, {dt:.1f} s"}
 
@@ -430,8 +473,9 @@ def main_dqn(args, rank, world, local, S, N, R, T):
         if coll and xk != "host":
             out["collective"] = coll
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_dqn(args.cpu_seconds, R=R, T=T)
-            out["cpu_baseline"].update(os_cpu_count=os.cpu_count(), threads=1)
+            out["cpu_baseline"] = cpu_baseline_all_cores("cpu_baseline_dqn", dict(seconds=args.cpu_seconds, R=R, T=T),
+                                                         cpu_workers())
+            out["cpu_baseline"].update(os_cpu_count=os.cpu_count())
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
@@ -440,16 +484,17 @@ def main_dqn(args, rank, world, local, S, N, R, T):
 
 
 def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 96, q_dtype: str = "f64",
-                 shared: bool = False, battery: bool = False, hetero: bool = False, t_sample: int = 0):
+                 shared: bool = False, battery: bool = False, hetero: bool = False, t_sample: int = 0,
+                 first: int = 0):
     """The oracle (NumPy CPU restatement, oracle/restatement.py) on a bounded sample of the same
     workload, single-threaded, Philox exploration.  t_sample > 0: episodes cut to the first
     t_sample slots of the generated horizon (per-step cost does not depend on T)."""
     from oracle.restatement import OracleBatch
     from p2pmicrogrid_amd.dataset import apply_asset_mix, asset_mix, scenario_batch
-    inp = scenario_batch(S, N, T)
+    inp = scenario_batch(S, N, T, first_scenario=first)
     lv, cap = None, (np.full((S, N), BATTERY_J) if battery else None)
     if hetero:
-        mix = asset_mix(S, N, battery_j=BATTERY_J)
+        mix = asset_mix(S, N, first_scenario=first, battery_j=BATTERY_J)
         inp, lv, cap = apply_asset_mix(inp, mix), mix.hp_levels, mix.battery_capacity
     full_T = T
     if t_sample and t_sample < T:
@@ -474,6 +519,7 @@ def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 
     if hetero:
         what = f"heterogeneous mixes + battery, first {T} of {full_T} slots, "
     return {"value": S * N * T * eps_done / dt, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "label": "CPU restatement (oracle/restatement.py)",
             "sample": f"{S} scenarios x N={N} (R={R}, T={T}, {what}{q_dtype} Q), {eps_done} training episodes, "
                       f"oracle/restatement.py vectorised NumPy, {dt:.1f} s"}
 
@@ -509,6 +555,7 @@ SIMDS = 256 * 4          # 256 CUs x 4 SIMDs
 # v_pk_fma_f32, two FMAs per lane).  Chip peak: one wave-instruction per SIMD per 4 cycles; a wave
 # that has its SIMD to itself issues at most that too (MI355X_MICROARCH.md 'ISSUE cost': 4 cycles).
 VALU_PEAK_G = SIMDS * CLOCK_GHZ / 4
+SQ_ENGINES = 32          # shader engines whose SQ_BUSY_CYCLES rocprofv3 sums (8 XCDs x 4)
 ONE_WAVE_PEAK_G = CLOCK_GHZ / 4
 
 
@@ -527,10 +574,20 @@ def issue_roofline(workload: str, kernel_ms: float):
     valu, waves = d["counters_per_launch"]["SQ_INSTS_VALU"], d["counters_per_launch"]["SQ_WAVES"]
     achieved = valu / (kernel_ms * 1e-3) / 1e9
     out = {"unit": "G VALU wave-instructions/s", "achieved": achieved, "peak": VALU_PEAK_G,
-           "frac": achieved / VALU_PEAK_G, "valu_insts_per_launch": valu, "waves": waves,
+           "frac": achieved / VALU_PEAK_G, "peak_clock_ghz": CLOCK_GHZ, "valu_insts_per_launch": valu, "waves": waves,
            "kernel": d.get("kernel"), "source": os.path.relpath(path, ROOT),
            # from the counter run itself: share of wave cycles issuing any instruction / waiting
            "active_frac": d["derived"].get("frac_active_inst_any"), "wait_frac": d["derived"].get("frac_wait_any")}
+    busy = d["counters_per_launch"].get("SQ_BUSY_CYCLES")
+    if busy:
+        # the same issue fraction at the clock the chip actually ran: SQ_BUSY_CYCLES is summed over
+        # the 32 shader engines, so busy / 32 = the launch's length in cycles (at the implied clock
+        # it matches the live kernel time); frac_busy_clock = VALU wave-instructions / (SIMDs x
+        # cycles / 4), independent of any clock assumption
+        cycles = busy / SQ_ENGINES
+        out["launch_cycles"] = cycles
+        out["frac_busy_clock"] = valu * 4.0 / (SIMDS * cycles)
+        out["implied_clock_ghz"] = cycles / (kernel_ms * 1e-3) / 1e9
     if waves <= SIMDS:  # one wave per SIMD at most: each wave is capped at one VALU per 4 cycles
         per_wave = achieved / waves
         out["one_wave_peak"] = ONE_WAVE_PEAK_G
@@ -538,14 +595,19 @@ def issue_roofline(workload: str, kernel_ms: float):
     return out
 
 
-def gather_roofline(n_agents: int, horizon: int, kernel_ms: float):
+def gather_roofline(n_agents: int, horizon: int, kernel_ms: float, stages: int = 1, agents_per_wave: int = 32,
+                    pool: int = 381, rows: int = 5, source: str = "r02_ubench_gather.jsonl"):
     """Dependent-gather floor of the per-agent-table fast kernel: the same geometry (one 5.12 MB
-    f64 table per agent, 32 agents per wave, 5 row gathers per step whose addresses depend on the
-    previous step's rows) with everything else stripped, timed by scripts/ubench_gather.hip
-    (profiles/r02_ubench_gather.jsonl, scripts/gpu_ubench_gather.sh).  frac = that floor over the
+    f64 table per agent, `agents_per_wave` agents per wave, row gathers whose addresses depend on
+    the previous step's rows) with everything else stripped, timed by scripts/ubench_gather.hip
+    (scripts/gpu_ubench_gather.sh).  configs[1]: one stage of 5 rows per step, 32 agents per wave
+    (profiles/r02_ubench_gather.jsonl).  configs[3]: two DEPENDENT stages per step (the round-0 and
+    next-state rows, then the round-1 row addressed from the partners' round-0 actions), 64 agents
+    per wave, 32,768 tables, a pool of 400 rows per agent (the oracle's year visits ~334 distinct
+    rows per agent in rounds 0-1) (profiles/r04_ubench_gather.jsonl).  frac = that floor over the
     live kernel time: how much of the episode is the memory round trip the reference's
     act -> T_in -> next-state dependency forces, and how much is the decision chain on top of it."""
-    path = os.path.join(ROOT, "profiles", "r02_ubench_gather.jsonl")
+    path = os.path.join(ROOT, "profiles", source)
     if not os.path.exists(path) or not kernel_ms == kernel_ms:
         return None
     for line in open(path):
@@ -553,8 +615,9 @@ def gather_roofline(n_agents: int, horizon: int, kernel_ms: float):
             d = json.loads(line)
         except Exception:  # noqa: BLE001
             continue
-        if (d.get("tables") == n_agents and d.get("steps") == horizon and d.get("rows_per_step") == 5
-                and d.get("agents_per_wave") == 32 and not d.get("pair_lanes") and d.get("pool_rows") == 381):
+        if (d.get("tables") == n_agents and d.get("steps") == horizon and d.get("rows_per_step") == rows
+                and d.get("stages", 1) == stages and d.get("agents_per_wave") == agents_per_wave
+                and not d.get("pair_lanes") and d.get("pool_rows") == pool):
             floor_us = d["kernel_us"]
             return {"unit": "us per launch", "floor": floor_us, "achieved": kernel_ms * 1e3,
                     "frac": floor_us / (kernel_ms * 1e3), "floor_cycles_per_step": d["cycles_per_step"],
@@ -771,15 +834,21 @@ def main():
                 out["roofline"]["gather_floor"] = gather
                 out["roofline"]["bound"] = "latency"  # one wave per CU: the dependent row-gather chain
                 out["roofline"]["binding_frac"] = gather["frac"]
+        elif hetero and q_dtype == "f64" and N == 4 and R == 1:
+            gather = gather_roofline(S * N, T, kernel_ms, stages=2, agents_per_wave=64, pool=400, rows=3,
+                                     source="r04_ubench_gather.jsonl")
+            if gather:  # two dependent gather round trips per step + the f64 battery rules on the chain
+                out["roofline"]["gather_floor"] = gather
+                out["roofline"]["bound"] = "latency"
+                out["roofline"]["binding_frac"] = gather["frac"]
         elif shared and issue and issue["frac"] > 0.5:
             out["roofline"]["bound"] = "valu-issue"  # every SIMD busy: VALU instructions per agent-step
             out["roofline"]["binding_frac"] = issue["frac"]
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(args.cpu_seconds, S=(64 if hetero else 256) if N <= 4 else 64,
-                              N=N, R=R, T=T, q_dtype=q_dtype, shared=shared, battery=battery,
-                              hetero=hetero, t_sample=960 if T > 960 else 0)
+            cb = cpu_baseline_all_cores("cpu_baseline", dict(
+                seconds=args.cpu_seconds, S=(64 if hetero else 256) if N <= 4 else 64, N=N, R=R, T=T, q_dtype=q_dtype,
+                shared=shared, battery=battery, hetero=hetero, t_sample=960 if T > 960 else 0), cpu_workers())
             cb["os_cpu_count"] = os.cpu_count()
-            cb["threads"] = 1  # NumPy here runs single-threaded element-wise ops (no BLAS on this path)
             if not (shared or battery or hetero):  # the per-object loop restates the tabular path only
                 cb["per_object"] = cpu_baseline_per_object(min(args.cpu_seconds, 5.0), N=N, R=R, T=T)
             out["cpu_baseline"] = cb

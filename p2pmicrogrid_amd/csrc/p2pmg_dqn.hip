@@ -412,8 +412,8 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
   const float b3 = th[kOffB3];
   // every round's exploration draw (or replayed code) ahead of the rounds: they depend only on
   // (t, episode, agent), so they run under the prologue's load latency, off the rounds' chain
-  uint64_t codes_pack = ~0ull;  // byte r: code of round r (255 = greedy), up to 8 rounds
-  if (agent_thr && !greedy_mode && R1 <= 8) {
+  uint64_t codes_pack = ~0ull;  // byte r: code of round r (255 = greedy); R + 1 <= kMaxRounds1 = 8 (p2pmg_create)
+  if (agent_thr && !greedy_mode) {
     if (p.rng == 0) {
       for (int w4 = 0; w4 < W; ++w4)
         codes_pack = (codes_pack & ~(0xFFFFFFFFull << (32 * w4))) |
@@ -450,19 +450,7 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
       for (int jj = 0; jj < N; ++jj) acc = acc + (-((jj == i) ? 0.0f : P[jj * N + i]));
       p2pf = div_n<N>(acc) / mi;
       code = 255;  // ActorModel.select_action rl.py:174-183: explore draw, else greedy
-      if (!greedy_mode) {
-        if (R1 <= 8) {
-          code = (int)((codes_pack >> (8 * r)) & 0xFFu);
-        } else if (p.rng == 0) {
-          code = (int)((p.codes[((size_t)t * W + (r >> 2)) * A + a] >> (8 * (r & 3))) & 0xFFu);
-        } else {
-          uint32_t c0 = (uint32_t)(t * ((R1 + 1) >> 1) + (r >> 1)), c1 = (uint32_t)p.episode,
-                   c2 = p.agent_offset + (uint32_t)a, c3 = kTagDecision;
-          philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-          const uint32_t wu = (r & 1) ? c2 : c0, wa = (r & 1) ? c3 : c1;
-          code = (double)wu * (1.0 / 4294967296.0) < p.eps ? (int)__umulhi(wa, 3u) : 255;
-        }
-      }
+      if (!greedy_mode) code = (int)((codes_pack >> (8 * r)) & 0xFFu);
       greedy = code == 255;
       shX[j] = make_float4(time_t, tnorm, bal, p2pf);
     }
@@ -538,10 +526,7 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
         else v = (jj == i) ? (tot == tot ? out * 0.0f : tot) : (out * fabsf(f[jj])) / tot;
         Pn[jj] = v;
       }
-      if (p.record & 32) {  // stored with the other records at the end (up to 8 rounds)
-        if (R1 <= 8) act_pack |= (uint64_t)act << (8 * r);
-        else p.rec_action[((size_t)t * R1 + r) * A + a] = (uint8_t)act;
-      }
+      if (p.record & 32) act_pack |= (uint64_t)act << (8 * r);  // stored with the other records at the end
     }
     __syncthreads();
     cur ^= 1;
@@ -672,7 +657,7 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
     if (p.record & 4) p.rec_grid[k] = g;
     if (p.record & 8) p.rec_p2p[k] = pp;
     if (p.record & 16) p.rec_tin[k] = tin0;
-    if ((p.record & 32) && R1 <= 8)
+    if (p.record & 32)
       for (int r = 0; r < R1; ++r) p.rec_action[((size_t)t * R1 + r) * A + a] = (uint8_t)(act_pack >> (8 * r));
     p.t_in[a] = tin;
     p.t_m[a] = tm;
@@ -1228,15 +1213,19 @@ __global__ void dqn_forward_kernel(const float* __restrict__ th, int n, const fl
 
 hipError_t launch_dqn_act(const DqnParams& d, hipStream_t st) {
   if (d.n_nets == 1 && !d.act_wave) {  // one shared network: AGW agents per workgroup on MFMA tiles
-#ifndef P2PMG_ACT_AGW
-#define P2PMG_ACT_AGW 16
-#endif
+    // AGW = 16 agent slots per workgroup (default), or 8 (d.act_agw, P2PMG_ACT_AGW=8: more, shorter
+    // workgroups; N <= 8 only) -- the same results bit for bit
     switch (d.e.N) {
-#define P2PMG_DQN_ACT_SHARED(NN)                                                                               \
-  case NN: {                                                                                                   \
-    constexpr int agw = NN <= 8 ? P2PMG_ACT_AGW : 16, spw = agw / NN;                                          \
-    hipLaunchKernelGGL((dqn_act_shared_kernel<NN, agw>), dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d); \
-    break;                                                                                                     \
+#define P2PMG_DQN_ACT_SHARED(NN)                                                                                     \
+  case NN: {                                                                                                         \
+    if (NN <= 8 && d.act_agw == 8) {                                                                                 \
+      constexpr int agw = NN <= 8 ? 8 : 16, spw = agw / NN;                                                          \
+      hipLaunchKernelGGL((dqn_act_shared_kernel<NN, agw>), dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d);     \
+    } else {                                                                                                         \
+      constexpr int spw = 16 / NN;                                                                                   \
+      hipLaunchKernelGGL((dqn_act_shared_kernel<NN, 16>), dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d);      \
+    }                                                                                                                \
+    break;                                                                                                           \
   }
       P2PMG_DQN_ACT_SHARED(1) P2PMG_DQN_ACT_SHARED(2) P2PMG_DQN_ACT_SHARED(3) P2PMG_DQN_ACT_SHARED(4)
       P2PMG_DQN_ACT_SHARED(5) P2PMG_DQN_ACT_SHARED(6) P2PMG_DQN_ACT_SHARED(7) P2PMG_DQN_ACT_SHARED(8)

@@ -93,6 +93,7 @@ struct DqnParams {
   float* smp;                // this step's sampled ring slots, int32 [A][32] (dqn_sample_kernel)
   int fused_sample;          // 1: dqn_act_kernel draws them (training env steps); 0: the sample kernel
   int act_wave;              // shared network: 1 = one wave per agent (dqn_act_kernel) instead of the MFMA act kernel
+  int act_agw;               // shared network, MFMA act kernel: agent slots per workgroup (16, or 8 for N <= 8)
   float* rec_loss;           // [T][A] or null
   float* ep_acc;             // [S] running sum_t mean_i r
   float gamma, tau, tau_c, lr_t, b1c, b2c, adam_eps, clip;

@@ -1686,6 +1686,8 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   {  // P2PMG_DQN_ACT=wave: the one-wave-per-agent act kernel for a shared network too (tests, A/B)
     const char* v = getenv("P2PMG_DQN_ACT");
     d.act_wave = (v && !strcmp(v, "wave")) ? 1 : 0;
+    const char* g = getenv("P2PMG_ACT_AGW");  // 8: the 8-slot MFMA act workgroups (tests, A/B)
+    d.act_agw = (g && atoi(g) == 8) ? 8 : 16;
   }
   c->last_kernel = std::string(c->n_nets == 1 && !d.act_wave ? "dqn_act_shared_kernel<" : "dqn_act_kernel<") +
                    std::to_string(c->N) + ">";

@@ -10,8 +10,14 @@
 // kernel touches ~380 distinct rows per agent per episode, ~100 MB over all 8192 tables); launches
 // repeat with the same pools, like the bench's back-to-back episodes, so L2 / MALL warm the same way.
 //
+// stages=2 is the configs[3] geometry (episode_fast_kernel<4, f64, 2, train, battery>): per step a
+// first stage of 2 rows (the round-0 row and the next-state row, both addressed from the previous
+// step's data), then a second, DEPENDENT stage of 1 row (the round-1 row, whose p2p bin follows from
+// the partners' round-0 actions, i.e. from the first stage's data); the next step's rows follow from
+// the second stage.  Two round trips per step, 64 agents per wave (16 scenarios x 4).
+//
 //   hipcc --offload-arch=gfx950 -O3 -o ubench_gather ubench_gather.hip
-//   ./ubench_gather [tables=8192] [pool=381] [rps=5] [steps=96] [lanes=32] [launches=20] [pair=0]
+//   ./ubench_gather [tables=8192] [pool=381] [rps=5] [steps=96] [lanes=32] [launches=20] [pair=0] [stages=1]
 // prints one JSON line: kernel us per launch (median of the last half), cycles per step (s_memtime of
 // each wave, averaged), the same with an L1-resident pool of 1 row (the ALU + L1 part of the step).
 #include <hip/hip_runtime.h>
@@ -97,6 +103,42 @@ __global__ __launch_bounds__(64) void chase(const char* __restrict__ q, int lane
   if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// two dependent gather stages per step: 2 rows, then 1 row addressed from their data (configs[3])
+__global__ __launch_bounds__(64) void chase2(const char* __restrict__ q, int lanes, uint32_t pool, int steps,
+                                             uint32_t* __restrict__ sink, unsigned long long* __restrict__ cyc) {
+  const int lane = (int)threadIdx.x;
+  const bool active = lane < lanes;
+  const uint32_t a = (uint32_t)(blockIdx.x * lanes + (active ? lane : 0));
+  const char* const qwave = q + (size_t)blockIdx.x * lanes * kStates * kRowBytes;
+  const uint32_t qlane = active ? (uint32_t)lane * kStates * kRowBytes : 0u;
+  uint32_t h = mix(a + 12345u);
+  uint32_t acc = 0;
+  unsigned long long t0;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int t = 0; t < steps; ++t) {
+    uint4 lo[2];
+    uint2 hi[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t k = (uint32_t)(((uint64_t)(h + (uint32_t)r * 97u) * pool) >> 32);
+      const char* p = qwave + (qlane + pool_row(a, k) * kRowBytes);
+      lo[r] = *reinterpret_cast<const uint4*>(p);
+      hi[r] = *reinterpret_cast<const uint2*>(p + 16);
+    }
+    const uint32_t x0 = mix((uint32_t)t ^ lo[0].x ^ lo[0].w ^ hi[0].y);  // round 0 -> the round-1 row
+    const uint32_t k1 = (uint32_t)(((uint64_t)x0 * pool) >> 32);
+    const char* p1 = qwave + (qlane + pool_row(a, k1) * kRowBytes);
+    const uint4 lo1 = *reinterpret_cast<const uint4*>(p1);
+    const uint2 hi1 = *reinterpret_cast<const uint2*>(p1 + 16);
+    h = mix(x0 ^ lo1.x ^ lo1.w ^ hi1.y ^ lo[1].y ^ hi[1].x);
+    acc += h;
+  }
+  unsigned long long t1;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  sink[blockIdx.x * 64 + lane] = acc;
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 template <int RPS, bool PAIR>
 static void run(const char* q, int blocks, int lanes, uint32_t pool, int steps, int launches, uint32_t* sink,
                 unsigned long long* cyc, double& us_med, double& cyc_step) {
@@ -109,7 +151,10 @@ static void run(const char* q, int blocks, int lanes, uint32_t pool, int steps, 
   int nc = 0;
   for (int l = 0; l < launches; ++l) {
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((chase<RPS, PAIR>), dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
+    if constexpr (RPS == 0)
+      hipLaunchKernelGGL(chase2, dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
+    else
+      hipLaunchKernelGGL((chase<RPS, PAIR>), dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms = 0.0f;
@@ -136,8 +181,10 @@ int main(int argc, char** argv) {
   const int lanes = argc > 5 ? atoi(argv[5]) : 32;
   const int launches = argc > 6 ? atoi(argv[6]) : 20;
   const bool pair = argc > 7 && atoi(argv[7]) != 0;
+  const int stages = argc > 8 ? atoi(argv[8]) : 1;
   if (tables <= 0 || lanes <= 0 || lanes > (pair ? 32 : 64) || tables % lanes || pool == 0 || steps <= 0 || launches < 2 ||
-      (size_t)lanes * kStates * kRowBytes >= (1ull << 32) || !(rps == 1 || rps == 5)) {
+      (size_t)lanes * kStates * kRowBytes >= (1ull << 32) || !(rps == 1 || rps == 5) || !(stages == 1 || stages == 2) ||
+      (stages == 2 && pair)) {
     fprintf(stderr, "bad arguments\n");
     return 2;
   }
@@ -152,7 +199,10 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_tables, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint32_t*>(q), bytes / 4, 7u);
   CK(hipDeviceSynchronize());
   double us = 0, cs = 0, us1 = 0, cs1 = 0;
-  if (rps == 5 && !pair) {
+  if (stages == 2) {
+    run<0, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
+    run<0, false>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
+  } else if (rps == 5 && !pair) {
     run<5, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
     run<5, false>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
   } else if (rps == 5) {
@@ -166,9 +216,9 @@ int main(int argc, char** argv) {
     run<1, true>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
   }
   printf("{\"probe\": \"ubench_gather\", \"tables\": %d, \"table_bytes\": %zu, \"pool_rows\": %u, \"rows_per_step\": %d, "
-         "\"steps\": %d, \"agents_per_wave\": %d, \"pair_lanes\": %d, \"waves\": %d, \"launches\": %d, \"kernel_us\": %.2f, "
-         "\"cycles_per_step\": %.1f, \"l1_pool1_kernel_us\": %.2f, \"l1_pool1_cycles_per_step\": %.1f}\n",
-         tables, bytes, pool, rps, steps, lanes, pair ? 1 : 0, blocks, launches, us, cs, us1, cs1);
+         "\"stages\": %d, \"steps\": %d, \"agents_per_wave\": %d, \"pair_lanes\": %d, \"waves\": %d, \"launches\": %d, "
+         "\"kernel_us\": %.2f, \"cycles_per_step\": %.1f, \"l1_pool1_kernel_us\": %.2f, \"l1_pool1_cycles_per_step\": %.1f}\n",
+         tables, bytes, pool, stages == 2 ? 3 : rps, stages, steps, lanes, pair ? 1 : 0, blocks, launches, us, cs, us1, cs1);
   CK(hipFree(q));
   CK(hipFree(sink));
   CK(hipFree(cyc));

@@ -300,15 +300,17 @@ def test_replay_samples_past_eviction_match_reference_fixture():
     eng.close()
 
 
-@pytest.mark.parametrize("S,N,R", [(37, 2, 1), (11, 3, 2), (5, 16, 1), (20, 1, 0), (9, 5, 1)])
-def test_shared_act_mfma_kernel_equals_wave_kernel(S, N, R, monkeypatch):
-    """A shared network's act launch on MFMA tiles (dqn_act_shared_kernel, 16 agents per workgroup,
-    partial last workgroup when 16 / N does not divide S) gives bitwise the records, replay rings,
-    sampled slots and trained weights of the one-wave-per-agent kernel (P2PMG_DQN_ACT=wave): same
-    fmaf chain over k in layer 2, same pairwise tree over the 64 units in layer 3; Philox and
-    replay-mode exploration and replay draws."""
+@pytest.mark.parametrize("S,N,R,agw", [(37, 2, 1, 16), (11, 3, 2, 16), (5, 16, 1, 16), (20, 1, 0, 16), (9, 5, 1, 16),
+                                      (6, 2, 7, 16), (37, 2, 1, 8), (11, 3, 7, 8), (9, 5, 1, 8)])
+def test_shared_act_mfma_kernel_equals_wave_kernel(S, N, R, agw, monkeypatch):
+    """A shared network's act launch on MFMA tiles (dqn_act_shared_kernel, 16 or 8 agent slots per
+    workgroup (P2PMG_ACT_AGW), partial last workgroup when the slots / N do not divide S, up to the
+    8-round maximum) gives bitwise the records, replay rings, sampled slots and trained weights of
+    the one-wave-per-agent kernel (P2PMG_DQN_ACT=wave): same fmaf chain over k in layer 2, same
+    pairwise tree over the 64 units in layer 3; Philox and replay-mode exploration and replay draws."""
     T = 24
     runs = []
+    monkeypatch.setenv("P2PMG_ACT_AGW", str(agw))
     for kind in ("wave", "mfma"):
         if kind == "wave":
             monkeypatch.setenv("P2PMG_DQN_ACT", "wave")
