@@ -1036,6 +1036,39 @@ __device__ __forceinline__ double qcore64(double n, const Recip64& r) {
 // [0, 2^10], |load|, |pv|, heat-pump levels <= 2^100).  Then every numerator is 0 or in
 // [2^-252, 2^168] (a positive SoC - bound difference is a multiple of the bound's ulp >= 2^-152; a
 // nonzero f32 balance times 900 lies in [2^-140, 2^138]) and the per-lane range tests go.
+// The SoC-only terms of the rule (storage.py:52-60: available energy / space, the full test), the
+// same for every round of a step: computed once per step (bat_pre) and shared by the rounds.
+struct BatPre {
+  double avail_energy, avail_space;
+  bool full;
+};
+// x / d for d > 0 and x >= +0: qcore64 without the sign fix, which only matters for x = -0
+__device__ __forceinline__ double qpos64(double n, const Recip64& r) {
+  const double q = n * r.y;
+  return __builtin_fma(__builtin_fma(-r.d, q, n), r.y, q);
+}
+__device__ __forceinline__ BatPre bat_pre(double soc, double cap, const BatK& b) {
+  // space >= +0 (fmax with 0, a positive capacity), so the unsigned quotient is the IEEE one
+  return BatPre{(fmax(0.0, soc - b.smin) * cap) * b.se, qpos64(fmax(0.0, b.smax - soc) * cap, b.rse), soc >= b.smax};
+}
+// battery_rule_r<false> on a step's precomputed SoC terms (the launcher-verified domain): every
+// quotient's numerator is positive where it is used (dis: x = min(energy, avail_energy) > 0;
+// chg: x = min(-energy, avail_space) > 0 as soc < smax), so the quotients need no sign fix
+__device__ __forceinline__ double battery_rule_pre(double balance, double& soc, const Recip64& rcap, const BatK& b,
+                                                   const BatPre& pr) {
+  const double energy = (balance * 60.0) * 15.0;
+  const bool dis = balance > 0.0 && pr.avail_energy > 0.0;
+  const bool chg = !dis && balance < 0.0 && !pr.full;
+  const double x = dis ? (energy <= pr.avail_energy ? energy : pr.avail_energy)    // min(energy, available_energy)
+                       : (-energy <= pr.avail_space ? -energy : pr.avail_space);  // min(-energy, available_space)
+  const double q1 = qpos64(x, rcap);     // x / capacity
+  const double q2 = qpos64(x, b.r900);   // x / 900
+  const double q3 = qpos64(q1, b.rse);   // (x / capacity) / sqrt(eff)
+  const double soc_n = dis ? soc - q3 : soc + b.se * q1;
+  const double bal_n = dis ? balance - q2 : balance + q2;
+  soc = (dis || chg) ? soc_n : soc;
+  return (dis || chg) ? bal_n : balance;
+}
 template <bool CHECK = true>
 __device__ __forceinline__ double battery_rule_r(double balance, double& soc, double cap, const Recip64& rcap,
                                                  const BatK& b) {
@@ -1086,6 +1119,9 @@ struct FastRec {         // [T][A], 32 B
   uint32_t bins;         // (it * nT*nb + ib) | iT << 16
   uint32_t ips;          // byte r: p2p bin of round r
 };
+#ifndef P2PMG_BAT_SPEC  // 1: the final round's battery rule for all 3 actions inside its row's round trip
+#define P2PMG_BAT_SPEC 0
+#endif
 // BAT: 0 none, 1 battery with per-lane range tests, 2 battery in the launcher-verified domain
 template <int N, typename QT, int R1, bool TRAIN, int BAT, bool NARROW>
 __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams p, const uint2* __restrict__ pre,
@@ -1342,8 +1378,14 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     }
     float out0 = balw + hp;
     double soc_r = soc;  // tentative SoC of the current round
+    BatPre bpre{};
+    if constexpr (BAT == 2) bpre = bat_pre(soc, bcap, bk);  // shared by the step's rounds
+    auto bat_rule = [&](float o, double& sr) -> float {
+      if constexpr (BAT == 2) return (float)battery_rule_pre((double)o, sr, rcap, bk, bpre);
+      return (float)battery_rule_r<true>((double)o, sr, bcap, rcap, bk);
+    };
     if constexpr (BAT != 0) {
-      if (bcap > 0.0) out0 = (float)battery_rule_r<BAT == 1>((double)out0, soc_r, bcap, rcap, bk);
+      if (bcap > 0.0) out0 = bat_rule(out0, soc_r);
     }
     const float ev0 = div_n_r<N>(out0 * 1.0f, rn);
 #pragma unroll
@@ -1386,6 +1428,22 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         rowR = gat((need ? strip + (uint32_t)ip : a0));
 #endif
       }
+#if P2PMG_BAT_SPEC
+      // the final round's battery rule for each of the 3 actions while its row is in flight (it
+      // needs only balw, the level and this step's SoC): the action then only selects
+      float outA[3];
+      double socA[3];
+      if constexpr (BAT != 0) {
+        if (r == R1 - 1) {
+#pragma unroll
+          for (int x = 0; x < 3; ++x) {
+            socA[x] = soc;
+            outA[x] = balw + hp_of(lv, x);
+            if (bcap > 0.0) outA[x] = bat_rule(outA[x], socA[x]);
+          }
+        }
+      }
+#endif
       act = code == 255 ? argmax3(rowR) : code;
       acts |= (uint32_t)act << (8 * r);
       ips |= (uint32_t)ip << (8 * r);
@@ -1410,8 +1468,17 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       }
       float out = balw + hp;
       if constexpr (BAT != 0) {
-        soc_r = soc;
-        if (bcap > 0.0) out = (float)battery_rule_r<BAT == 1>((double)out, soc_r, bcap, rcap, bk);
+#if P2PMG_BAT_SPEC
+        if (r == R1 - 1) {
+          const Sel3M m = sel3_masks(act);
+          out = sel3(m, outA[0], outA[1], outA[2]);
+          soc_r = sel3(m, socA[0], socA[1], socA[2]);
+        } else
+#endif
+        {
+          soc_r = soc;
+          if (bcap > 0.0) out = bat_rule(out, soc_r);
+        }
       }
 #if P2PMG_ABLATE == 11  // timing-only: no final-round divide-power and no market (cost from out alone)
       if (r == R1 - 1) {
@@ -1836,8 +1903,14 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     uint32_t acts = (uint32_t)act, ips = (uint32_t)ip_zero;
     double soc_r = soc;
     float out = balw + hp;
+    BatPre bpre{};
+    if constexpr (BAT == 2) bpre = bat_pre(soc, bcap, bk);  // shared by the step's two rounds
+    auto bat_rule = [&](float o, double& sr) -> float {
+      if constexpr (BAT == 2) return (float)battery_rule_pre((double)o, sr, rcap, bk, bpre);
+      return (float)battery_rule_r<true>((double)o, sr, bcap, rcap, bk);
+    };
     if constexpr (BAT != 0) {
-      if (bcap > 0.0) out = (float)battery_rule_r<BAT == 1>((double)out, soc_r, bcap, rcap, bk);
+      if (bcap > 0.0) out = bat_rule(out, soc_r);
     }
     const float ev0 = div_n<N>(out * 1.0f);
     const bool ok_ev0 = in_range19(ev0);
@@ -1868,7 +1941,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
       out = balw + hp;
       soc_r = soc;
       if constexpr (BAT != 0) {
-        if (bcap > 0.0) out = (float)battery_rule_r<BAT == 1>((double)out, soc_r, bcap, rcap, bk);
+        if (bcap > 0.0) out = bat_rule(out, soc_r);
       }
       const float flo = out < 0.0f ? 0.0f : -__builtin_inff(), fhi = out > 0.0f ? 0.0f : __builtin_inff();
       float f[N];
