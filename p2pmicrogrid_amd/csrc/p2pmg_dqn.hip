@@ -177,7 +177,7 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
                  c2 = p.agent_offset + (uint32_t)a, c3 = kTagDecision;
         philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
         const uint32_t wu = (r & 1) ? c2 : c0, wa = (r & 1) ? c3 : c1;
-        code = (double)wu * (1.0 / 4294967296.0) < p.eps ? (int)__umulhi(wa, 3u) : 255;
+        code = (p.eps_all || wu < p.eps_thr) ? (int)__umulhi(wa, 3u) : 255;  // wu / 2^32 < eps
       }
     }
     if (code == 255) {
@@ -423,8 +423,8 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
         uint32_t c0 = (uint32_t)(t * ((R1 + 1) >> 1) + q), c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
                  c3 = kTagDecision;
         philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-        const uint64_t k0 = (double)c0 * (1.0 / 4294967296.0) < p.eps ? __umulhi(c1, 3u) : 255u;
-        const uint64_t k1 = (double)c2 * (1.0 / 4294967296.0) < p.eps ? __umulhi(c3, 3u) : 255u;
+        const uint64_t k0 = (p.eps_all || c0 < p.eps_thr) ? __umulhi(c1, 3u) : 255u;  // c0 / 2^32 < eps
+        const uint64_t k1 = (p.eps_all || c2 < p.eps_thr) ? __umulhi(c3, 3u) : 255u;
         codes_pack = (codes_pack & ~(0xFFFFull << (16 * q))) | (k0 << (16 * q)) | (k1 << (16 * q + 8));
       }
     }

@@ -29,6 +29,10 @@ struct EpisodeParams {
   void* q;                   // [A][n_states][kQPad] f64 | f32
   const uint32_t* codes;     // [T][W][A] code words, W = ceil((R+1)/4), one byte per round (255 = greedy)
   double eps;
+  // explore test u < eps of a Philox word w (u = w / 2^32, exact) as an integer compare:
+  // eps_all || w < eps_thr (eps_threshold below, set with eps)
+  uint32_t eps_thr;
+  int eps_all;
   uint32_t seed_lo, seed_hi;
   uint32_t agent_offset;     // global id of local agent 0 (Philox counter)
   float* rec_reward;         // [T][A]
@@ -129,7 +133,17 @@ struct PrepOut {
   uint32_t* words; // [T][W][A] or null (no Philox draws)
   int episode;
   double eps;      // the epsilon its Philox draws are for
+  uint32_t eps_thr;  // its integer threshold (eps_threshold)
+  int eps_all;
 };
+// w / 2^32 < eps  <=>  w < ceil(eps * 2^32) for every 32-bit w (w / 2^32 and eps * 2^32 are exact in
+// f64): thr = that ceiling, clamped to [0, 2^32]; all = (thr == 2^32), when every w explores
+inline void eps_threshold(double eps, uint32_t& thr, int& all) {
+  double c = __builtin_ceil(eps * 4294967296.0);
+  if (!(c > 0.0)) c = 0.0;  // eps <= 0 or NaN: never
+  all = c >= 4294967296.0 ? 1 : 0;
+  thr = all ? 0xFFFFFFFFu : (uint32_t)c;
+}
 hipError_t launch_step_prepass(const EpisodeParams& p, const PrepOut& o, hipStream_t stream);
 // next != null: the launch also runs the step pre-pass of the next episode (episode p.episode + 1,
 // same epsilon) into *next, in extra workgroups beside the episode's own

@@ -319,8 +319,8 @@ __device__ __forceinline__ uint32_t philox_code_pair(const EpisodeParams& p, int
   uint32_t c0 = (uint32_t)(t * pairs + pair), c1 = (uint32_t)p.episode, c2 = gid, c3 = kTagDecision;
   philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
   const uint32_t a0 = (uint32_t)(((uint64_t)c1 * 3ull) >> 32), a1 = (uint32_t)(((uint64_t)c3 * 3ull) >> 32);
-  const uint32_t k0 = (double)c0 * (1.0 / 4294967296.0) < p.eps ? a0 : 255u;
-  const uint32_t k1 = (double)c2 * (1.0 / 4294967296.0) < p.eps ? a1 : 255u;
+  const uint32_t k0 = (p.eps_all || c0 < p.eps_thr) ? a0 : 255u;  // c0 / 2^32 < eps
+  const uint32_t k1 = (p.eps_all || c2 < p.eps_thr) ? a1 : 255u;
   return k0 | (k1 << 8);
 }
 __device__ __forceinline__ uint32_t philox_code(const EpisodeParams& p, int t, int r, uint32_t gid) {
@@ -933,6 +933,8 @@ __device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOu
     EpisodeParams q = p;
     q.episode = o.episode;
     q.eps = o.eps;
+    q.eps_thr = o.eps_thr;
+    q.eps_all = o.eps_all;
     const int R1 = p.R + 1, W = (R1 + 3) >> 2;
     for (int w = 0; w < W; ++w) {
       uint32_t word = 0xFFFFFFFFu;

@@ -594,6 +594,7 @@ static EpisodeParams episode_params(p2pmg_ctx* c, const p2pmg_episode_args* args
   p.q = c->q;
   p.codes = c->codes;
   p.eps = args->epsilon;
+  p2pmg::eps_threshold(p.eps, p.eps_thr, p.eps_all);
   if (train && args->rng == P2PMG_RNG_PHILOX) p.rng = 1;  // in-kernel unless the pre-pass below runs
   p.seed_lo = (uint32_t)(g.seed & 0xFFFFFFFFu);
   p.seed_hi = (uint32_t)(g.seed >> 32);
@@ -712,7 +713,7 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
                      (!philox || (c->spec_episode[ps] == args->episode && c->spec_eps[ps] == args->epsilon));
     if (!hit) {
       const p2pmg::PrepOut o{c->pre[ps], p.pre_ipc, philox ? c->pcodes[ps] : nullptr, args->episode,
-                             args->epsilon};
+                             args->epsilon, p.eps_thr, p.eps_all};
       HIP_TRY(c, p2pmg::launch_step_prepass(p, o, c->stream));
     }
     // the next slot, for episode + 1 at the caller's next epsilon (the decay schedule is known,
@@ -725,7 +726,8 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     const bool have_next = (args->flags & P2PMG_FLAG_NEXT_EPSILON) != 0 || args->next_epsilon > 0.0;
     const double next_eps = have_next ? args->next_epsilon : args->epsilon;
     next = p2pmg::PrepOut{c->pre[ns], want_ipc ? c->pre_ipc[ns] : nullptr, philox ? c->pcodes[ns] : nullptr,
-                          args->episode + 1, next_eps};
+                          args->episode + 1, next_eps, 0u, 0};
+    p2pmg::eps_threshold(next_eps, next.eps_thr, next.eps_all);
     produce = !env_no_spec;
     if (hit) c->spec_hits++;
     else c->spec_misses++;

@@ -303,8 +303,9 @@ class DeviceCommunityBatch:
         return out[:n.value].copy()
 
     def collective_ms(self):
-        """(total ms, count) of the data-path RCCL all-reduces (shared-table delta, DQN gradient)
-        since the last reset_kernel_times (HIP events on the context's stream; syncs)."""
+        """(total ms, count) of the data-path RCCL collectives (shared-table delta all-reduce, DQN
+        gradient-segment all-gather) since the last reset_kernel_times, every call counted (HIP
+        events on the context's stream; syncs)."""
         ms, n = C.c_double(0.0), C.c_int(0)
         self._chk(self.L.p2pmg_collective_ms(self._ctx, C.byref(ms), C.byref(n)), "collective_ms")
         return float(ms.value), int(n.value)

@@ -9,8 +9,12 @@ worst=0
 for step in "$@"; do
   name="${step%%|*}"; rest="${step#*|}"; to="${rest%%|*}"; cmd="${rest#*|}"
   echo "== $name ($to s): $cmd"
+  # heartbeat: a long, quiet step (a CPU-side oracle check) still shows progress every 60 s
+  ( while sleep 60; do echo "$(date +%T) $name running" >> "$D/heartbeat.txt"; done ) &
+  hb=$!
   timeout -k 10 "$to" bash -c "$cmd" > "$D/$name.out" 2> "$D/$name.err"
   rc=$?
+  kill "$hb" 2>/dev/null; wait "$hb" 2>/dev/null
   echo "== $name rc=$rc"; tail -3 "$D/$name.out"
   if [ $rc -eq 124 ] || [ $rc -ge 128 ]; then echo "fatal rc $rc at $name: stopping"; exit $rc; fi
   [ $rc -ne 0 ] && worst=$rc
