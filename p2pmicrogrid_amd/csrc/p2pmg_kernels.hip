@@ -1122,7 +1122,7 @@ struct FastRec {         // [T][A], 32 B
   uint32_t ips;          // byte r: p2p bin of round r
 };
 #ifndef P2PMG_BAT_SPEC  // 1: the final round's battery rule for all 3 actions inside its row's round trip
-#define P2PMG_BAT_SPEC 0
+#define P2PMG_BAT_SPEC 1  // configs[3] 59.6 -> 58.7 ms (profiles/r04_battery_ab.txt)
 #endif
 // BAT: 0 none, 1 battery with per-lane range tests, 2 battery in the launcher-verified domain
 template <int N, typename QT, int R1, bool TRAIN, int BAT, bool NARROW>

@@ -18,6 +18,8 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -o ubench_gather ubench_gather.hip
 //   ./ubench_gather [tables=8192] [pool=381] [rps=5] [steps=96] [lanes=32] [launches=20] [pair=0] [stages=1]
+// stages=3: the prefetch study (chase_pf): kernel_us / cycles_per_step without the prefetch, the
+// l1_pool1_* fields WITH it (same pool)
 // prints one JSON line: kernel us per launch (median of the last half), cycles per step (s_memtime of
 // each wave, averaged), the same with an L1-resident pool of 1 row (the ALU + L1 part of the step).
 #include <hip/hip_runtime.h>
@@ -139,6 +141,70 @@ __global__ __launch_bounds__(64) void chase2(const char* __restrict__ q, int lan
   if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// configs[1] with a one-step-ahead prefetch (stages=3 selects it; PF = 0 measures the same access
+// pattern without the prefetch): each step's 5 rows are one of 3 candidate sets, picked by a 2-bit
+// choice from the previous step's data (the final action: which of 3 next temperature bins).  With
+// PF, a step first touches every candidate set of the NEXT step (15 dword loads, results unused, issued
+// after this step's own rows so the in-order wait for those does not wait for them), so by the time the
+// choice is known the chosen rows are in L2 -- if the candidates can be known a step ahead, as the
+// next T_in / bins for each action are in episode_fast_kernel.
+template <bool PF>
+__global__ __launch_bounds__(64) void chase_pf(const char* __restrict__ q, int lanes, uint32_t pool, int steps,
+                                               uint32_t* __restrict__ sink, unsigned long long* __restrict__ cyc) {
+  const int lane = (int)threadIdx.x;
+  const bool active = lane < lanes;
+  const uint32_t a = (uint32_t)(blockIdx.x * lanes + (active ? lane : 0));
+  const char* const qwave = q + (size_t)blockIdx.x * lanes * kStates * kRowBytes;
+  const uint32_t qlane = active ? (uint32_t)lane * kStates * kRowBytes : 0u;
+  // candidate set c of step t: rows pool_row(a, k) with k = hash(t, c, r) (known ahead; the choice is not)
+  auto row_of = [&](int t, uint32_t c, int r) {
+    const uint32_t k = (uint32_t)(((uint64_t)mix((uint32_t)t * 0x9E3779B9u + c * 0x632BE5ABu + (uint32_t)r * 97u) * pool) >> 32);
+    return qwave + (qlane + pool_row(a, k) * kRowBytes);
+  };
+  uint32_t choice = mix(a) % 3u;
+  uint32_t acc = 0;
+  unsigned long long t0;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  uint4 lo[5];
+  uint2 hi[5];
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const char* p = row_of(0, choice, r);
+    lo[r] = *reinterpret_cast<const uint4*>(p);
+    hi[r] = *reinterpret_cast<const uint2*>(p + 16);
+  }
+  for (int t = 0; t < steps; ++t) {
+    if (PF && t + 1 < steps) {  // touch every candidate row of step t + 1
+#pragma unroll
+      for (uint32_t c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+          uint32_t dummy;
+          asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(row_of(t + 1, c, r)) : "memory");
+        }
+    }
+    uint32_t x = (uint32_t)t;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) x ^= lo[r].x ^ lo[r].w ^ hi[r].y;
+    const uint32_t h = mix(x);
+    acc += h;
+    choice = h % 3u;  // the final action picks the next step's candidate set
+    if (t + 1 < steps) {
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {
+        const char* p = row_of(t + 1, choice, r);
+        lo[r] = *reinterpret_cast<const uint4*>(p);
+        hi[r] = *reinterpret_cast<const uint2*>(p + 16);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned long long t1;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  sink[blockIdx.x * 64 + lane] = acc;
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 template <int RPS, bool PAIR>
 static void run(const char* q, int blocks, int lanes, uint32_t pool, int steps, int launches, uint32_t* sink,
                 unsigned long long* cyc, double& us_med, double& cyc_step) {
@@ -153,6 +219,10 @@ static void run(const char* q, int blocks, int lanes, uint32_t pool, int steps, 
     CK(hipEventRecord(e0));
     if constexpr (RPS == 0)
       hipLaunchKernelGGL(chase2, dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
+    else if constexpr (RPS == -1)
+      hipLaunchKernelGGL(chase_pf<false>, dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
+    else if constexpr (RPS == -2)
+      hipLaunchKernelGGL(chase_pf<true>, dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
     else
       hipLaunchKernelGGL((chase<RPS, PAIR>), dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
     CK(hipEventRecord(e1));
@@ -183,8 +253,8 @@ int main(int argc, char** argv) {
   const bool pair = argc > 7 && atoi(argv[7]) != 0;
   const int stages = argc > 8 ? atoi(argv[8]) : 1;
   if (tables <= 0 || lanes <= 0 || lanes > (pair ? 32 : 64) || tables % lanes || pool == 0 || steps <= 0 || launches < 2 ||
-      (size_t)lanes * kStates * kRowBytes >= (1ull << 32) || !(rps == 1 || rps == 5) || !(stages == 1 || stages == 2) ||
-      (stages == 2 && pair)) {
+      (size_t)lanes * kStates * kRowBytes >= (1ull << 32) || !(rps == 1 || rps == 5) || stages < 1 || stages > 4 ||
+      (stages >= 2 && pair)) {
     fprintf(stderr, "bad arguments\n");
     return 2;
   }
@@ -202,6 +272,9 @@ int main(int argc, char** argv) {
   if (stages == 2) {
     run<0, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
     run<0, false>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
+  } else if (stages == 3) {  // 3 candidate sets per step, no prefetch (us) / with prefetch (us1)
+    run<-1, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
+    run<-2, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us1, cs1);
   } else if (rps == 5 && !pair) {
     run<5, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
     run<5, false>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
