@@ -1770,6 +1770,7 @@ __device__ __forceinline__ pkf2 fdiv_core_pk(pkf2 a, pkf2 b, pkf2 y) {
 #define P2PMG_SQ16_OCC 4  // min waves per SIMD the register allocation must allow (LDS allows 4)
 #endif
 constexpr int kSq16Waves = 8;                        // waves per workgroup (one hash per 32 scenarios)
+constexpr int kEpWin = 8;                            // steps per episode-reward window (sq16)
 constexpr int kTpStride = 16 * 16 + 16;              // floats per scenario tile (+16: bank offset)
 // BAT: 0 none, 1 battery with per-lane range tests, 2 battery in the launcher-verified domain
 template <typename QT, int R1, bool TRAIN, int BAT, bool NARROW>
@@ -1778,6 +1779,12 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   __shared__ uint32_t hkey[kSqSlots];
   __shared__ unsigned long long hval[kSqSlots];
   __shared__ __attribute__((aligned(16))) float tpall[kSq16Waves * SPW * kTpStride];
+  // avg_reward = sum_t mean_i r (community.py:179) in windows of kEpWin steps: the rewards of a
+  // window land in [step][agent]; at its end lane i sums step i's row (the agents in order, as
+  // before) and the scenario's running sum takes the window's step means in step order.  One row
+  // sum per lane per window instead of a 16-add row sum in every lane every step.
+  __shared__ __attribute__((aligned(16))) float rwin[kSq16Waves * SPW][kEpWin][N];
+  __shared__ __attribute__((aligned(16))) float mwin[kSq16Waves * SPW][kEpWin];
   const int wv = (int)(threadIdx.x / kWave);
   const int lane = (int)(threadIdx.x % kWave);
   const int sl = lane / G;
@@ -2043,17 +2050,24 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
       rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
     }
     rec_ptr += rec_step;
-    // avg_reward = sum_t mean_i r (community.py:179): the group's rewards in agent order
-    tp[i] = rw;
-    wave_lds_fence();
-    float msum = 0.0f;
+    // avg_reward = sum_t mean_i r (community.py:179): the group's rewards in agent order, per window
+    float* const rw_sc = &rwin[wv * SPW + sl][0][0];
+    rw_sc[(t % kEpWin) * N + i] = rw;
+    if (t % kEpWin == kEpWin - 1 || t + 1 == T) {
+      const int nw = t % kEpWin + 1;  // steps in this window (uniform)
+      wave_lds_fence();
+      float msum = 0.0f;
+      const float* row = rw_sc + (i % kEpWin) * N;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const float4 v = *reinterpret_cast<const float4*>(tp + 4 * m);
-      msum = msum + v.x; msum = msum + v.y; msum = msum + v.z; msum = msum + v.w;
+      for (int m = 0; m < 4; ++m) {
+        const float4 v = *reinterpret_cast<const float4*>(row + 4 * m);
+        msum = msum + v.x; msum = msum + v.y; msum = msum + v.z; msum = msum + v.w;
+      }
+      if (i < kEpWin) mwin[wv * SPW + sl][i] = div_n<N>(msum);
+      wave_lds_fence();
+      for (int q = 0; q < nw; ++q) ep_sum = ep_sum + mwin[wv * SPW + sl][q];
+      wave_lds_fence();
     }
-    wave_lds_fence();
-    ep_sum = ep_sum + div_n<N>(msum);
     if constexpr (TRAIN) {
       if (t % kSqFlushSteps == kSqFlushSteps - 1 || t + 1 == T)
         lds_hash_flush(hkey, hval, dbase, kSq16Waves * kWave);

@@ -1,12 +1,15 @@
 #!/bin/bash
-# Round-3 profile refresh at HEAD: the bench line of every workload (with its CPU baseline), the
+# A round's profile refresh at HEAD: the bench line of every workload (with its CPU baseline), the
 # launcher's --gpus 2 rehearsal, rocprofv3 kernel stats, FETCH_SIZE / WRITE_SIZE in separate --pmc
 # passes for the configs[1], [2], [3] episode kernels, SQ counter passes (configs[1], [2]) and the
-# instruction-rate microbenchmark.  Stops at the first failure.  scripts/summarize_r03.py -> profiles/.
-# usage: gpu_refresh_r03.sh [A|B]  (A: bench lines, microbenchmark, kernel stats; B: PMC + SQ passes)
+# instruction-rate microbenchmark.  Stops at the first failure.  scripts/summarize_refresh.py ROUND
+# -> profiles/.
+# usage: gpu_refresh.sh ROUND [A|B]  (e.g. r04 A: bench lines, microbenchmark, kernel stats;
+#        B: PMC + SQ passes)
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
-O="$R/gpurun_out/r03"; mkdir -p "$O"
-PART="${1:-A}"
+RND="${1:-r04}"
+O="$R/gpurun_out/$RND"; mkdir -p "$O"
+PART="${2:-A}"
 run() {  # name timeout args...
   local n=$1 to=$2; shift 2
   timeout -k 10 "$to" python -u bench.py "$@" > "$O/$n.json" 2> "$O/$n.err" || { tail -20 "$O/$n.err"; exit 1; }

@@ -205,6 +205,76 @@ __global__ __launch_bounds__(64) void chase_pf(const char* __restrict__ q, int l
   if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// configs[1] as a LEAD-1 pipeline (stages=4): the next step's rows depend on this step's final action
+// only through 3 options (the next T_in per heat-pump level), so all 3 candidate sets of step t + 1
+// (3 x 5 rows) are loaded at the START of step t, a whole step before they are needed; step t then
+// waits only for its own sets (loaded during step t - 1) and picks one by the previous step's choice.
+// No dependent round trip remains on the step: the step time is the issue / memory-pipeline cost of
+// 30 scattered loads per lane and step.  Registers: 2 x 15 rows.
+__global__ __launch_bounds__(64) void chase_lead(const char* __restrict__ q, int lanes, uint32_t pool, int steps,
+                                                 uint32_t* __restrict__ sink, unsigned long long* __restrict__ cyc) {
+  const int lane = (int)threadIdx.x;
+  const bool active = lane < lanes;
+  const uint32_t a = (uint32_t)(blockIdx.x * lanes + (active ? lane : 0));
+  const char* const qwave = q + (size_t)blockIdx.x * lanes * kStates * kRowBytes;
+  const uint32_t qlane = active ? (uint32_t)lane * kStates * kRowBytes : 0u;
+  // option x of step t on the known state `base`: pool slot k = (hash(t, base) + 37 x + 7 r) mod pool,
+  // row = (rowbase + 311 k) mod 20^4: a few ALU ops per row, like the kernel's strip + bin offsets
+  // (one hash per step and option set, not per row)
+  const uint32_t rowbase = pool_row(a, 0);
+  auto row_of = [&](int t, uint32_t base, uint32_t x, int r) {
+    const uint32_t th = mix((uint32_t)t * 0x9E3779B9u + base * 0x27D4EB2Fu);
+    const uint32_t k = (th + x * 37u + (uint32_t)r * 7u) & (pool - 1u);  // pool: a power of two <= 512
+    const uint32_t row = rowbase + k * 311u;                               // < 2 x 20^4
+    return qwave + (qlane + (row >= kStates ? row - kStates : row) * kRowBytes);
+  };
+  uint32_t c = mix(a) % 3u, base = mix(a + 7u);
+  uint32_t acc = 0;
+  uint4 loA[3][5], loB[3][5];
+  uint2 hiA[3][5], hiB[3][5];
+  auto load_sets = [&](uint4 (&lo)[3][5], uint2 (&hi)[3][5], int t, uint32_t b) {
+#pragma unroll
+    for (uint32_t x = 0; x < 3; ++x)
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {
+        const char* p = row_of(t, b, x, r);
+        lo[x][r] = *reinterpret_cast<const uint4*>(p);
+        hi[x][r] = *reinterpret_cast<const uint2*>(p + 16);
+      }
+  };
+  auto use_set = [&](uint4 (&lo)[3][5], uint2 (&hi)[3][5], int t) {
+    // the chosen set by masks, so every loaded value is consumed (a select would let the compiler
+    // sink the three loads into one load of the selected address: a dependent gather again)
+    const uint32_t m0 = 0u - (uint32_t)(c == 0), m1 = 0u - (uint32_t)(c == 1), m2 = 0u - (uint32_t)(c == 2);
+    uint32_t x = (uint32_t)t;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      x ^= ((lo[0][r].x ^ lo[0][r].w ^ hi[0][r].y) & m0) | ((lo[1][r].x ^ lo[1][r].w ^ hi[1][r].y) & m1) |
+           ((lo[2][r].x ^ lo[2][r].w ^ hi[2][r].y) & m2);
+    }
+    const uint32_t hsh = mix(x);
+    acc += hsh;
+    base = base * 31u + c;  // the state the next options hang on (known once c is)
+    c = hsh % 3u;
+  };
+  unsigned long long t0;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  load_sets(loA, hiA, 0, base);
+  int t = 0;
+  for (; t + 2 <= steps; t += 2) {
+    load_sets(loB, hiB, t + 1, base * 31u + c);  // step t + 1's options, issued before step t's wait
+    use_set(loA, hiA, t);
+    if (t + 2 < steps) load_sets(loA, hiA, t + 2, base * 31u + c);
+    use_set(loB, hiB, t + 1);
+  }
+  if (t < steps) use_set(loA, hiA, t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned long long t1;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  sink[blockIdx.x * 64 + lane] = acc;
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 template <int RPS, bool PAIR>
 static void run(const char* q, int blocks, int lanes, uint32_t pool, int steps, int launches, uint32_t* sink,
                 unsigned long long* cyc, double& us_med, double& cyc_step) {
@@ -223,6 +293,8 @@ static void run(const char* q, int blocks, int lanes, uint32_t pool, int steps, 
       hipLaunchKernelGGL(chase_pf<false>, dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
     else if constexpr (RPS == -2)
       hipLaunchKernelGGL(chase_pf<true>, dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
+    else if constexpr (RPS == -3)
+      hipLaunchKernelGGL(chase_lead, dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
     else
       hipLaunchKernelGGL((chase<RPS, PAIR>), dim3(blocks), dim3(64), 0, 0, q, lanes, pool, steps, sink, cyc);
     CK(hipEventRecord(e1));
@@ -275,6 +347,13 @@ int main(int argc, char** argv) {
   } else if (stages == 3) {  // 3 candidate sets per step, no prefetch (us) / with prefetch (us1)
     run<-1, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
     run<-2, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us1, cs1);
+  } else if (stages == 4) {  // the lead-1 pipeline (us) and the same with an L1-resident pool (us1)
+    if ((pool & (pool - 1)) || pool > 512) {
+      fprintf(stderr, "stages=4: pool must be a power of two <= 512\n");
+      return 2;
+    }
+    run<-3, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
+    run<-3, false>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);
   } else if (rps == 5 && !pair) {
     run<5, false>(q, blocks, lanes, pool, steps, launches, sink, cyc, us, cs);
     run<5, false>(q, blocks, lanes, 1u, steps, launches, sink, cyc, us1, cs1);

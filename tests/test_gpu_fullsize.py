@@ -119,11 +119,13 @@ def test_full_size_config5_dqn_per_agent_sampled_oracle():
         for k in ("reward", "cost", "grid", "p2p", "t_in"):
             assert np.array_equal(got[k][:, pick], out[k]), (e, k)
         if mode == "train":
-            _rel_close(eng.get_record("loss")[:, pick], out["loss"], rtol=1e-4)
+            # the kernel-order oracle: losses bit for bit
+            assert np.array_equal(eng.get_record("loss")[:, pick], out["loss"])
             # properties over every agent of the batch
             assert np.all(np.isfinite(eng.get_record("loss")))
         assert np.all(got["action"] <= 2) and np.all(got["p2p"].sum(axis=-1) == 0)
     th = eng.get_weights("online")[agents]
+    assert np.array_equal(th, ob.theta) and np.array_equal(eng.get_weights("adam_v")[agents], ob.v)
     _rel_close(th - th0[agents], ob.theta - th0[agents], rtol=1e-2, floor=1e-2)
     eng.close()
 
@@ -156,5 +158,20 @@ def test_full_size_config5_dqn_shared_network_properties(monkeypatch):
     assert np.array_equal(wa, wb) and np.all(np.isfinite(wa))
     assert not np.array_equal(wa, w0)  # 2 x 96 Adam steps moved the network
     assert a.step == 2 * T
-    a.close()
     b.close()
+    # 8 sampled scenarios of a greedy day of the full-size launch against the kernel-order oracle
+    # (ActorModel.greedy_action's Q values, act_q), with the network the full batch trained
+    pick = np.sort(np.random.RandomState(5).choice(S, 8, replace=False))
+    t_in, t_m = (x.reshape(S, N) for x in a.get_temperatures())
+    ob = odqn.OracleDQNBatch(S=len(pick), N=N, R=R, load_w=inp.load_w[pick], pv_w=inp.pv_w[pick],
+                             max_in=inp.max_in[pick], env_time=inp.time[None], env_tout=inp.t_out[pick],
+                             theta0=wa, shared=True)
+    ob.t_in, ob.t_m = t_in[pick].copy(), t_m[pick].copy()
+    keys = ("reward", "cost", "grid", "p2p", "t_in", "action")
+    a.run_episode("greedy", record=keys)
+    got = a.get_records(keys)
+    out = ob.run_episode("greedy")
+    assert np.array_equal(got["action"][:, :, pick], out["action"].astype(np.uint8))
+    for k in ("reward", "cost", "grid", "p2p", "t_in"):
+        assert np.array_equal(got[k][:, pick], out[k]), k
+    a.close()
