@@ -376,15 +376,6 @@ __device__ __forceinline__ Row4<QT> sel_row(int b, const Row4<QT>& x0, const Row
   return r;
 }
 template <typename QT>
-__device__ __forceinline__ Row4<QT> sel_row_m(const Sel3M& m, const Row4<QT>& x0, const Row4<QT>& x1,
-                                              const Row4<QT>& x2) {
-  Row4<QT> r;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) r.v[k] = sel3(m, x0.v[k], x1.v[k], x2.v[k]);
-  r.v[3] = (QT)0;
-  return r;
-}
-template <typename QT>
 __device__ __forceinline__ Row4<QT> patched(Row4<QT> r, uint32_t addr, const Patch<QT>& pt) {
   if (pt.row == addr) {
 #pragma unroll
@@ -1130,9 +1121,6 @@ struct FastRec {         // [T][A], 32 B
   uint32_t bins;         // (it * nT*nb + ib) | iT << 16
   uint32_t ips;          // byte r: p2p bin of round r
 };
-#ifndef P2PMG_LEAD  // 1: N = 2 candidate path as a lead-1 pipeline (step t + 1's rows for all 3 final actions)
-#define P2PMG_LEAD 0
-#endif
 #ifndef P2PMG_BAT_SPEC  // 1: the final round's battery rule for all 3 actions inside its row's round trip
 #define P2PMG_BAT_SPEC 1  // configs[3] 59.6 -> 58.7 ms (profiles/r04_battery_ab.txt)
 #endif
@@ -1155,14 +1143,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   // pre-pass wrote; all three are issued a step ahead, so round 1 waits for no gather
   // (not with a battery: the partner's round-0 power then depends on its state of charge)
   constexpr bool CAND = N == 2 && R1 >= 2 && BAT == 0;
-  // LEAD: the next step's rows depend on this step's final action only through 3 options (the next
-  // T_in per heat-pump level, stA / nrA below), so all 3 options' rows of step t + 1 are issued at the
-  // START of step t and step t waits only for its own (issued a step earlier), then picks the option
-  // of the previous step's final action: no dependent gather round trip left on the step
-  constexpr bool LEAD = CAND && P2PMG_LEAD;
-#if P2PMG_TRACE
-  static_assert(!LEAD, "the step trace covers the dependent-gather layout only");
-#endif
   const int lane = (int)threadIdx.x;
   const int sl = lane / G;
   const int i = lane % G;
@@ -1274,19 +1254,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
 #pragma unroll
     for (int b = 0; b < 3; ++b) cand[b] = gat((strip + ((iS[0] >> (8 * b)) & 0xFFu)));
   }
-  // LEAD: the rows of one step for each option of the previous final action, in 3 slots (slot P of the
-  // 3-step unroll holds step t's, slot P + 1 receives step t + 1's: no register copies)
-  Row4<QT> LR0[LEAD ? 3 : 1][3], LCN[LEAD ? 3 : 1][3][3], LRN[LEAD ? 3 : 1][3];
-  int aprev = 0;  // LEAD: the previous step's final action (option of this step's rows)
-  if constexpr (LEAD) {
-#pragma unroll
-    for (int x = 0; x < 3; ++x) {
-      LR0[0][x] = row0;
-      LRN[0][x] = rowN;
-#pragma unroll
-      for (int b = 0; b < 3; ++b) LCN[0][x][b] = cand[b];
-    }
-  }
   Patch<QT> pat{0xFFFFFFFFu, 0, (QT)0};
   float ep_sum = 0.0f;
 #if P2PMG_TRACE  // timing-only probe: per-step s_memtime splits of one wave, printed at the end
@@ -1324,28 +1291,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
         stA[x] = strip_of(p1.y & 0xFFFFu, (int)iTA[x]);
         nrA[x] = strip_of(p1.y >> 16, (int)iTA[x]) + (uint32_t)ip_zero;
       }
-    }
-    if constexpr (LEAD) {
-      // step t + 1's rows for each final action x of this step, before this step's rows are waited
-      // for; the round-0 row only where step t + 1's round 0 is greedy (as issue_next does)
-      const uint32_t cwn = code_of(c1);
-      const bool g0 = (cwn & 0xFF) == 255;
-#pragma unroll
-      for (int x = 0; x < 3; ++x) {
-        Row4<QT> r0{};
-        if (g0) r0 = gat(row0_addr(stA[x], nrA[x], cwn));
-        LR0[P1][x] = r0;
-#pragma unroll
-        for (int b = 0; b < 3; ++b) LCN[P1][x][b] = gat(stA[x] + ((ipc1 >> (8 * b)) & 0xFFu));
-      }
-#pragma unroll
-      for (int x = 0; x < 3; ++x) LRN[P1][x] = gat(TRAIN ? nrA[x] : row0_addr(stA[x], nrA[x], cwn));
-      // this step's rows: the option the previous step's final action took
-      const Sel3M mp = sel3_masks(aprev);
-      row0 = sel_row_m(mp, LR0[P][0], LR0[P][1], LR0[P][2]);
-#pragma unroll
-      for (int b = 0; b < 3; ++b) cand[b] = sel_row_m(mp, LCN[P][0][b], LCN[P][1][b], LCN[P][2][b]);
-      rowN = sel_row_m(mp, LRN[P][0], LRN[P][1], LRN[P][2]);
     }
     // Between the rows' arrival and the next step's gathers the wave issues on the critical path
     // (the gathers' latency is the rest of the step): only what those addresses need goes there;
@@ -1392,10 +1337,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       cw1 = code_of(c1);
       a0n = row0_addr(strip1, nrow1, cw1);
       aNn = TRAIN ? nrow1 : a0n;
-      if constexpr (LEAD) {
-        aprev = act_final;  // step t + 1's rows are in flight since this step's start
-        return;
-      }
 #if P2PMG_ABLATE == 8 || P2PMG_ABLATE == 10
       row0n = fake_row(q + a0n * kQPad);
       rowNn = fake_row(q + aNn * kQPad);
@@ -1829,7 +1770,6 @@ __device__ __forceinline__ pkf2 fdiv_core_pk(pkf2 a, pkf2 b, pkf2 y) {
 #define P2PMG_SQ16_OCC 4  // min waves per SIMD the register allocation must allow (LDS allows 4)
 #endif
 constexpr int kSq16Waves = 8;                        // waves per workgroup (one hash per 32 scenarios)
-constexpr int kEpWin = 8;                            // steps per episode-reward window (sq16)
 constexpr int kTpStride = 16 * 16 + 16;              // floats per scenario tile (+16: bank offset)
 // BAT: 0 none, 1 battery with per-lane range tests, 2 battery in the launcher-verified domain
 template <typename QT, int R1, bool TRAIN, int BAT, bool NARROW>
@@ -1838,12 +1778,6 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   __shared__ uint32_t hkey[kSqSlots];
   __shared__ unsigned long long hval[kSqSlots];
   __shared__ __attribute__((aligned(16))) float tpall[kSq16Waves * SPW * kTpStride];
-  // avg_reward = sum_t mean_i r (community.py:179) in windows of kEpWin steps: the rewards of a
-  // window land in [step][agent]; at its end lane i sums step i's row (the agents in order, as
-  // before) and the scenario's running sum takes the window's step means in step order.  One row
-  // sum per lane per window instead of a 16-add row sum in every lane every step.
-  __shared__ __attribute__((aligned(16))) float rwin[kSq16Waves * SPW][kEpWin][N];
-  __shared__ __attribute__((aligned(16))) float mwin[kSq16Waves * SPW][kEpWin];
   const int wv = (int)(threadIdx.x / kWave);
   const int lane = (int)(threadIdx.x % kWave);
   const int sl = lane / G;
@@ -2109,24 +2043,17 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
       rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
     }
     rec_ptr += rec_step;
-    // avg_reward = sum_t mean_i r (community.py:179): the group's rewards in agent order, per window
-    float* const rw_sc = &rwin[wv * SPW + sl][0][0];
-    rw_sc[(t % kEpWin) * N + i] = rw;
-    if (t % kEpWin == kEpWin - 1 || t + 1 == T) {
-      const int nw = t % kEpWin + 1;  // steps in this window (uniform)
-      wave_lds_fence();
-      float msum = 0.0f;
-      const float* row = rw_sc + (i % kEpWin) * N;
+    // avg_reward = sum_t mean_i r (community.py:179): the group's rewards in agent order
+    tp[i] = rw;
+    wave_lds_fence();
+    float msum = 0.0f;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const float4 v = *reinterpret_cast<const float4*>(row + 4 * m);
-        msum = msum + v.x; msum = msum + v.y; msum = msum + v.z; msum = msum + v.w;
-      }
-      if (i < kEpWin) mwin[wv * SPW + sl][i] = div_n<N>(msum);
-      wave_lds_fence();
-      for (int q = 0; q < nw; ++q) ep_sum = ep_sum + mwin[wv * SPW + sl][q];
-      wave_lds_fence();
+    for (int m = 0; m < 4; ++m) {
+      const float4 v = *reinterpret_cast<const float4*>(tp + 4 * m);
+      msum = msum + v.x; msum = msum + v.y; msum = msum + v.z; msum = msum + v.w;
     }
+    wave_lds_fence();
+    ep_sum = ep_sum + div_n<N>(msum);
     if constexpr (TRAIN) {
       if (t % kSqFlushSteps == kSqFlushSteps - 1 || t + 1 == T)
         lds_hash_flush(hkey, hval, dbase, kSq16Waves * kWave);

@@ -2,7 +2,7 @@
 # A round's profile refresh at HEAD: the bench line of every workload (with its CPU baseline), the
 # launcher's --gpus 2 rehearsal, rocprofv3 kernel stats, FETCH_SIZE / WRITE_SIZE in separate --pmc
 # passes for the configs[1], [2], [3] episode kernels, SQ counter passes (configs[1], [2]) and the
-# instruction-rate microbenchmark.  Stops at the first failure.  scripts/summarize_refresh.py ROUND
+# instruction-rate microbenchmark, and an MFMA-busy pass over configs[4].  Stops at the first failure.  scripts/summarize_refresh.py ROUND
 # -> profiles/.
 # usage: gpu_refresh.sh ROUND [A|B]  (e.g. r04 A: bench lines, microbenchmark, kernel stats;
 #        B: PMC + SQ passes)
@@ -57,4 +57,8 @@ for W in config2 config3; do
     timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace -d "$O/sq/${W}_$P" -o p --output-format csv -- python3 "$R/bench.py" --workload $W --steps $ST --warmup 1 --no-cpu-baseline > "$O/sq_${W}_$P.log" 2>&1 || { tail -20 "$O/sq_${W}_$P.log"; exit 1; }
   done
 done
+# configs[4]: the DQN kernels' MFMA busy cycles beside the clock (SQ_BUSY_CYCLES) and the VALU / LDS
+# issue that shares the SIMDs with the MFMA stream
+PC="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU"
+timeout -s KILL 240 rocprofv3 --pmc $PC --kernel-trace -d "$O/sq/config5_C" -o p --output-format csv -- python3 "$R/bench.py" --workload config5 --steps 2 --warmup 1 --no-cpu-baseline > "$O/sq_config5_C.log" 2>&1 || { tail -20 "$O/sq_config5_C.log"; exit 1; }
 echo done

@@ -14,11 +14,12 @@ import os
 import sys
 
 out_dir = sys.argv[1]
-KERNEL = {"config2": "episode_fast_kernel", "config3": "episode_sq16_kernel"}
+KERNEL = {"config2": "episode_fast_kernel", "config3": "episode_sq16_kernel", "config5": "dqn_train_kernel"}
+SQ_ENGINES = 32  # SQ_BUSY_CYCLES sums the shader engines' busy cycles (bench.py issue roofline)
 res = {}
 for w, kname in KERNEL.items():
     agg = collections.defaultdict(list)
-    for p in ("A", "B"):
+    for p in ("A", "B", "C"):
         files = glob.glob(os.path.join(out_dir, f"{w}_{p}", "**", "*counter_collection.csv"), recursive=True)
         if not files:
             continue
@@ -47,7 +48,11 @@ for w, kname in KERNEL.items():
         "lds_per_wave": d.get("SQ_INSTS_LDS", 0) / waves,
         # one wave alone issues a VALU every 4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost')
         "valu_issue_frac_of_one_wave_peak": (4 * d.get("SQ_INSTS_VALU", 0) / (4 * wc)) if wc else None,
+        "launch_cycles": d.get("SQ_BUSY_CYCLES", 0) / SQ_ENGINES,
     }
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in d and d.get("SQ_BUSY_CYCLES"):
+        # MFMA-busy cycles summed over the 1024 SIMDs, over the SIMD-cycles of the launch
+        der["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * der["launch_cycles"])
     res[w] = {"kernel": kname, "workload": w, "counters_per_launch": d, "derived": der,
               "source": "scripts/gpu_sq_counters.sh (rocprofv3 --pmc, two passes of <= 8 SQ counters, P2PMG_NO_SPEC=1)"}
     if len(sys.argv) > 2:
