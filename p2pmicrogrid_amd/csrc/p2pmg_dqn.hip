@@ -759,40 +759,17 @@ __device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const f
   do {               \
   } while (0)
 #endif
-// train workgroups per CU (waves per SIMD) of the shared-network kernel: 2 in the default build
-// (about 220 VGPRs); 3 with -DP2PMG_TRAIN_OCC=3 (<= 168 VGPRs, the LW layout below).  The
-// per-agent-network kernel keeps 2 (about 200 VGPRs)
+// train workgroups per CU (waves per SIMD): 2 in the default build (about 220 VGPRs)
 #ifndef P2PMG_TRAIN_OCC
 #define P2PMG_TRAIN_OCC 2
 #endif
-// The shared network at 3 waves per SIMD (LW): 60 fewer VGPRs than the 2-wave layout.
-//   * the target W2 lives in LDS (16 KB, XOR-swizzled so a layer-2 operand read is conflict-free)
-//     instead of 16 registers per lane; the layer-3 vectors (b2, W3 of both networks) too;
-//   * the target tiles' layer-1 activations are not stored: the 32 rows' pre-activations of
-//     features 0..3 are (the 3 action values share them), and layer 2 forms each operand as
-//     relu(fmaf(action, W1[4][k], z) + b1[k]) -- the same single-rounding ops the 2-wave layout
-//     stores, so the same bits; dZ2 then reuses that array (its last reader is layer 2);
-//   * the backward issues dW2's products before it reads dH1's operands.
-// LDS 43.5 KB per workgroup (3 x 43.5 KB per CU).
-#ifndef P2PMG_TRAIN_LW
-#define P2PMG_TRAIN_LW (P2PMG_TRAIN_OCC >= 3)
-#endif
-constexpr bool kTrainLw = P2PMG_TRAIN_LW;
 template <bool SHARED>
-__global__ __launch_bounds__(256, SHARED ? P2PMG_TRAIN_OCC : 2) void dqn_train_kernel(const DqnParams d) {
-  constexpr bool LW = SHARED && kTrainLw;
+__global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const DqnParams d) {
   __shared__ float smpb[2][kB * kTrans];  // this agent's batch and the next one's (prefetched)
-  // target layer-1 activations (96 rows: action x sample), or (LW) the 32 rows' pre-activations
-  __shared__ __attribute__((aligned(16))) float H1t[LW ? kB : 3 * kB][kLdsRow];
+  __shared__ float H1t[3 * kB][kLdsRow];
   __shared__ __attribute__((aligned(16))) float H1oT[kH][kLdsRowT];  // online layer-1 activations, unit-major
-  __shared__ __attribute__((aligned(16))) float dZ2x[LW ? 1 : kB][kLdsRow];
-  float (*const dZ2)[kLdsRow] = LW ? H1t : dZ2x;
+  __shared__ __attribute__((aligned(16))) float dZ2[kB][kLdsRow];
   __shared__ float qpart[4][4 * kB];  // per-wave partial Q: rows 0..95 target (action x sample), 96..127 online
-  // LW: target W2[k][j] at k * 64 + (j ^ 16 (k & 3)); {W1[4][k], b1[k]} of the target; the layer-3
-  // vectors b2t, W3t, b2o, W3o (64 floats each, read as float4 per 4 units)
-  __shared__ float W2l[LW ? kH * kH : 1];
-  __shared__ float2 WB1[LW ? kH : 1];
-  __shared__ __attribute__((aligned(16))) float L3[LW ? 4 * kH : 4];
   const EpisodeParams& p = d.e;
   const int w = threadIdx.x / kWave, l = threadIdx.x % kWave;
   const int c16 = l & 15, g4 = l >> 4;
@@ -816,32 +793,16 @@ __global__ __launch_bounds__(256, SHARED ? P2PMG_TRAIN_OCC : 2) void dqn_train_k
   TrainW W;
   // one shared network: the lane's 48 W2 operands (layer 2: W2[4 kk + g4][col] of the target and
   // the online network; dH1: W2[col][4 kk + g4]) stay in registers for the whole launch
-  // (LW: the target's 16 in LDS instead)
-  float w2t[SHARED && !LW ? 16 : 1], w2o[SHARED ? 16 : 1], w2c[SHARED ? 16 : 1];
+  float w2t[SHARED ? 16 : 1], w2o[SHARED ? 16 : 1], w2c[SHARED ? 16 : 1];
   if constexpr (SHARED) {
     const float* th0 = d.theta + (size_t)net * kNetStride;
     const float* tg0 = d.target + (size_t)net * kNetStride;
     load_train_w(W, th0, tg0, col, g4, h0);
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
-      if constexpr (!LW) w2t[kk] = tg0[kOffW2 + (4 * kk + g4) * kH + col];
+      w2t[kk] = tg0[kOffW2 + (4 * kk + g4) * kH + col];
       w2o[kk] = th0[kOffW2 + (4 * kk + g4) * kH + col];
       w2c[kk] = th0[kOffW2 + col * kH + 16 * g4 + kk];  // dH1's K order: unit 16 g4 + kk
-    }
-    if constexpr (LW) {
-#pragma unroll
-      for (int m = 0; m < kH * kH / 256; ++m) {
-        const int e = m * 256 + (int)threadIdx.x, kr = e / kH, j = e % kH;
-        W2l[kr * kH + (j ^ (16 * (kr & 3)))] = tg0[kOffW2 + e];
-      }
-      if (threadIdx.x < kH) {
-        const int u = (int)threadIdx.x;
-        WB1[u] = make_float2(tg0[kOffW1 + 4 * kH + u], tg0[kOffB1 + u]);
-        L3[u] = tg0[kOffB2 + u];
-        L3[kH + u] = tg0[kOffW3 + u];
-        L3[2 * kH + u] = th0[kOffB2 + u];
-        L3[3 * kH + u] = th0[kOffW3 + u];
-      }
     }
   }
   // the first agent's batch (explicit batch, or the sample pre-pass output)
@@ -885,39 +846,29 @@ __global__ __launch_bounds__(256, SHARED ? P2PMG_TRAIN_OCC : 2) void dqn_train_k
     __builtin_amdgcn_s_setprio(2);  // MFMA phase (see layer 2)
     // all products first (8 independent accumulators), then the bias / ReLU / LDS stores: no store
     // waits on the MFMA it follows
-    // (the target tiles of one data row tile are the same product for the 3 action values: LW
-    // computes the two distinct ones; the 2-wave layout's six are CSE'd to the same two)
-    constexpr int kZT = LW ? 2 : 6;
-    f32x4 z1[kZT + 2];
+    f32x4 z1[8];
 #pragma unroll
-    for (int rt = 0; rt < kZT; ++rt) {
+    for (int rt = 0; rt < 6; ++rt) {
       const int b = (16 * rt + c16) % kB;
       z1[rt] = mfma4(smp[b][6 + g4], bt0, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
     }
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) z1[kZT + rt] = mfma4(smp[16 * rt + c16][g4], bo0, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+    for (int rt = 0; rt < 2; ++rt) z1[6 + rt] = mfma4(smp[16 * rt + c16][g4], bo0, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) z1[kZT + rt] = mfma4(g4 == 0 ? smp[16 * rt + c16][4] : 0.0f, bo1, z1[kZT + rt]);
+    for (int rt = 0; rt < 2; ++rt) z1[6 + rt] = mfma4(g4 == 0 ? smp[16 * rt + c16][4] : 0.0f, bo1, z1[6 + rt]);
     // a target tile holds one action value (rows 16 rt .. + 15: action rt / 2), so its K = 4 term
     // is a per-column fmaf, the same single rounding as an MFMA's second product would give
-    if constexpr (LW) {
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < 6; ++rt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) H1t[16 * rt + 4 * g4 + r][col] = z1[rt][r];
-    } else {
-#pragma unroll
-      for (int rt = 0; rt < 6; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          H1t[16 * rt + 4 * g4 + r][col] = relu(fmaf((rt >> 1) == 0 ? 0.0f : ((rt >> 1) == 1 ? 0.5f : 1.0f), W.w14t, z1[rt][r]) + b1t);
-    }
+      for (int r = 0; r < 4; ++r)
+        H1t[16 * rt + 4 * g4 + r][col] = relu(fmaf((rt >> 1) == 0 ? 0.0f : ((rt >> 1) == 1 ? 0.5f : 1.0f), W.w14t, z1[rt][r]) + b1t);
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
       float h[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float z = z1[kZT + rt][r] + b1o;
+        const float z = z1[6 + rt][r] + b1o;
         h[r] = relu(z);
         if (z > 0.0f) z1mask |= 1u << (4 * rt + r);
       }
@@ -940,48 +891,18 @@ __global__ __launch_bounds__(256, SHARED ? P2PMG_TRAIN_OCC : 2) void dqn_train_k
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt) at[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     ao[0] = ao[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    const float* const w2row = W2l + 16 * (w ^ g4) + c16;  // LW: + k * 64 is W2t[k][col] (k & 3 = g4)
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const int k = 4 * kk + g4;
+      const float bt = SHARED ? w2t[SHARED ? kk : 0] : tg[kOffW2 + k * kH + col];
       const float bo = SHARED ? w2o[SHARED ? kk : 0] : th[kOffW2 + k * kH + col];
-      if constexpr (LW) {
-        const float bt = w2row[k * kH];
-        const float2 wb = WB1[k];
-        const float zr[2] = {H1t[c16][k], H1t[16 + c16][k]};
 #pragma unroll
-        for (int rt = 0; rt < 6; ++rt) {
-          const float act = (rt >> 1) == 0 ? 0.0f : ((rt >> 1) == 1 ? 0.5f : 1.0f);
-          at[rt] = mfma4(bt, relu(fmaf(act, wb.x, zr[rt & 1]) + wb.y), at[rt]);
-        }
-      } else {
-        const float bt = SHARED ? w2t[SHARED && !LW ? kk : 0] : tg[kOffW2 + k * kH + col];
-#pragma unroll
-        for (int rt = 0; rt < 6; ++rt) at[rt] = mfma4(bt, H1t[16 * rt + c16][k], at[rt]);
-      }
+      for (int rt = 0; rt < 6; ++rt) at[rt] = mfma4(bt, H1t[16 * rt + c16][k], at[rt]);
       ao[0] = mfma4(bo, H1oT[k][c16], ao[0]);
       ao[1] = mfma4(bo, H1oT[k][16 + c16], ao[1]);
-      if (LW && (kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bounds the operand reads in flight
     }
     __builtin_amdgcn_s_setprio(0);
     DQN_STAMP(2);
-    // LW: the next agent's batch goes to the other buffer here, not at the end: its registers are
-    // then free before the backward (the register peak)
-    if (LW && has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
-    // LW: this lane's layer-3 vectors (units h0 .. h0 + 3)
-    f32x4 l3v[LW ? 4 : 1];
-    if constexpr (LW) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) l3v[m] = *reinterpret_cast<const f32x4*>(&L3[m * kH + h0]);
-    }
-    float b2t[4], w3t[4], b2o[4], w3o[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      b2t[r] = LW ? l3v[0][r] : W.b2t[r];
-      w3t[r] = LW ? l3v[LW ? 1 : 0][r] : W.w3t[r];
-      b2o[r] = LW ? l3v[LW ? 2 : 0][r] : W.b2o[r];
-      w3o[r] = LW ? l3v[LW ? 3 : 0][r] : W.w3o[r];
-    }
     // ---- layer 3, this wave's 16 units: in-lane over r (a pairwise tree), then over the 4 row
     // groups for four tiles at once (reduce4_groups: 3 lane swaps + 3 adds, row group g4 ends with
     // tile tag4's sum), so every lane stores one value per four tiles, without a masked branch
@@ -990,7 +911,7 @@ __global__ __launch_bounds__(256, SHARED ? P2PMG_TRAIN_OCC : 2) void dqn_train_k
     for (int rt = 0; rt < 6; ++rt) {
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = relu(at[rt][r] + b2t[r]) * w3t[r];
+      for (int r = 0; r < 4; ++r) v[r] = relu(at[rt][r] + W.b2t[r]) * W.w3t[r];
       s8[rt] = (v[0] + v[1]) + (v[2] + v[3]);
     }
     float h2o[2][4];
@@ -1000,10 +921,10 @@ __global__ __launch_bounds__(256, SHARED ? P2PMG_TRAIN_OCC : 2) void dqn_train_k
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float z = ao[rt][r] + b2o[r];
+        const float z = ao[rt][r] + W.b2o[r];
         h2o[rt][r] = relu(z);
         if (z > 0.0f) z2mask |= 1u << (4 * rt + r);
-        v[r] = h2o[rt][r] * w3o[r];
+        v[r] = h2o[rt][r] * W.w3o[r];
       }
       s8[6 + rt] = (v[0] + v[1]) + (v[2] + v[3]);
     }
@@ -1055,7 +976,7 @@ __global__ __launch_bounds__(256, SHARED ? P2PMG_TRAIN_OCC : 2) void dqn_train_k
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const bool on = (z2mask >> (4 * rt + r)) & 1u;
-        dz2[r] = on ? dq[rt] * w3o[r] : 0.0f;
+        dz2[r] = on ? dq[rt] * W.w3o[r] : 0.0f;
         gW3[r] += h2o[rt][r] * dq[rt];
         gb2[r] += dz2[r];
       }
@@ -1082,44 +1003,35 @@ __global__ __launch_bounds__(256, SHARED ? P2PMG_TRAIN_OCC : 2) void dqn_train_k
     for (int q = 0; q < 8; ++q) db[q] = dZ2[8 * g4 + q][col];
     // dH1 = dZ2 W2^T (own columns n = col) in the K order unit 16 g4 + kk: A = dZ2[16 rt + c16][16 g4
     // .. + 15] (four 16-B reads per rt), B = W2[col][16 g4 + kk] (registers for a shared network)
-    if constexpr (LW) {  // register budget: dW2's products issue before dH1's operands are read
+#if P2PMG_TRAIN_OCC >= 3  // register budget: dW2's products issue before dH1's operands are read
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+    for (int q = 0; q < 8; ++q)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) gW2[mt] = mfma4(ha[mt][q], db[q], gW2[mt]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+      for (int mt = 0; mt < 4; ++mt) gW2[mt] = mfma4(ha[mt][q], db[q], gW2[mt]);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     float za[2][16];
-    auto read_za = [&](int v) __attribute__((always_inline)) {
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
         const float4 u = *reinterpret_cast<const float4*>(&dZ2[16 * rt + c16][16 * g4 + 4 * v]);
         za[rt][4 * v] = u.x; za[rt][4 * v + 1] = u.y; za[rt][4 * v + 2] = u.z; za[rt][4 * v + 3] = u.w;
       }
-    };
-    // LW reads each group of four just ahead of its products (register budget); else all up front
-#pragma unroll
-    for (int v = 0; v < 4; ++v)
-      if (!LW || v == 0) read_za(v);
     // dW1's A operand: input feature c16 (< 5) of data rows b = 16 rt + 4 g4 + r (lanes c16 >= 5 read
     // feature 4 and select 0: no exec-masked read)
-    if constexpr (!LW) {
+#if P2PMG_TRAIN_OCC < 3
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+    for (int q = 0; q < 8; ++q)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) gW2[mt] = mfma4(ha[mt][q], db[q], gW2[mt]);
-    }
+      for (int mt = 0; mt < 4; ++mt) gW2[mt] = mfma4(ha[mt][q], db[q], gW2[mt]);
+#endif
     f32x4 acc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
+    for (int kk = 0; kk < 16; ++kk)
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt)
         acc[rt] = mfma4(za[rt][kk], SHARED ? w2c[SHARED ? kk : 0] : th[kOffW2 + col * kH + 16 * g4 + kk], acc[rt]);
-      if (LW && (kk & 3) == 3 && kk < 15) {
-        read_za(kk / 4 + 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
     // dZ1 = dH1 * [z1 > 0]; dW1 = X^T dZ1 (two accumulators: independent chains)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -1134,7 +1046,7 @@ __global__ __launch_bounds__(256, SHARED ? P2PMG_TRAIN_OCC : 2) void dqn_train_k
         for (int k = 0; k < 5; ++k) gx1[k] = fmaf(xr[k], dz1, gx1[k]);
       }
     __builtin_amdgcn_s_setprio(0);
-    if (!LW && has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
+    if (has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
     DQN_STAMP(5);
     __syncthreads();  // every wave is done with this agent's LDS and with the online W2
     DQN_STAMP(1);
