@@ -39,10 +39,18 @@ def needs_build() -> bool:
 
 
 KERNEL_PARTS = 9  # p2pmg_kernels.hip is compiled once per part (-DP2PMG_PART=k), see its header
+# Per-part compiler flags.  Part 5 (episode_sq16_kernel, VALU-issue-bound) without the SLP vectorizer:
+# SLP packs adjacent f32 adds / muls into v_pk_add_f32 / v_pk_mul_f32, which issue at 6.6 SIMD cycles
+# against 2 x 2.9 / 2 x 2.6 for the scalar pair at 4 waves per SIMD (profiles/r04_ubench_rate.jsonl);
+# the kernel's explicit packed FMAs (v_pk_fma_f32, 6.8 against 2 x 3.8) stay.  configs[2] 3.18 ->
+# 3.07 ms; the latency-bound fast kernel (other parts) measured slower without SLP
+# (profiles/r04_sq16_slp_ab.txt).
+PART_FLAGS = {5: ["-fno-slp-vectorize"]}
 
 
 def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=(), jobs: int = 0) -> str:
-    """defines: extra -D flags (timing-only ablation builds go to a different ``out``).
+    """defines: extra -D flags, or raw compiler flags when they start with "-" (timing-only ablation
+    builds go to a different ``out``).
     The translation units (9 parts of p2pmg_kernels.hip, p2pmg_dqn.hip, p2pmg_runtime.cpp) compile
     in parallel into build/obj/<tag>/, then link into one shared library.  An exclusive file lock
     per tag serialises concurrent builders (torchrun ranks, pytest-xdist workers that all find the
@@ -65,8 +73,8 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=(),
 def _build_locked(obj_dir: str, out: str, defines, jobs: int, verbose: bool) -> str:
     common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
               "-Wall", "-Wno-unused-function", "-Wno-pass-failed", f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
-              *[f"-D{d}" for d in defines]]
-    units = [(os.path.join(CSRC, "p2pmg_kernels.hip"), [f"-DP2PMG_PART={k}"], f"kernels_{k}.o")
+              *[d if d.startswith("-") else f"-D{d}" for d in defines]]  # "-..." entries: raw flags
+    units = [(os.path.join(CSRC, "p2pmg_kernels.hip"), [f"-DP2PMG_PART={k}", *PART_FLAGS.get(k, [])], f"kernels_{k}.o")
              for k in range(KERNEL_PARTS)]
     units += [(os.path.join(CSRC, s), [], os.path.splitext(s)[0] + ".o") for s in SOURCES if s != "p2pmg_kernels.hip"]
     jobs = jobs or min(len(units), max(1, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))

@@ -67,6 +67,38 @@ __global__ __launch_bounds__(256) void rate(unsigned* out, unsigned a, unsigned 
                       : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3) : "v"(b));)
     } else if constexpr (K == 14) {
       X4(asm volatile("v_mul_hi_u32_u24 %0, %0, %4\n v_mul_hi_u32_u24 %1, %1, %4\n v_mul_hi_u32_u24 %2, %2, %4\n v_mul_hi_u32_u24 %3, %3, %4"
+                      : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3) : "v"(b));)    } else if constexpr (K == 15) {
+      X4(asm volatile("v_fma_f32 %0, %0, %4, %4\n v_fma_f32 %1, %1, %4, %4\n v_fma_f32 %2, %2, %4, %4\n v_fma_f32 %3, %3, %4, %4"
+                      : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3) : "v"(fb));)
+    } else if constexpr (K == 16 || K == 17) {
+      typedef float f2t __attribute__((ext_vector_type(2)));
+      f2t p0 = {f0, f1}, p1 = {f2, f3}, p2 = {f1, f0}, p3 = {f3, f2}, pb = {fb, fb};
+      if constexpr (K == 16) {
+        X4(asm volatile("v_pk_add_f32 %0, %0, %4\n v_pk_add_f32 %1, %1, %4\n v_pk_add_f32 %2, %2, %4\n v_pk_add_f32 %3, %3, %4"
+                        : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3) : "v"(pb));)
+      } else {
+        X4(asm volatile("v_pk_mul_f32 %0, %0, %4\n v_pk_mul_f32 %1, %1, %4\n v_pk_mul_f32 %2, %2, %4\n v_pk_mul_f32 %3, %3, %4"
+                        : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3) : "v"(pb));)
+      }
+      f0 = p0.x + p1.y + p2.x + p3.y;
+    } else if constexpr (K == 18) {
+      X4(asm volatile("v_mul_f32 %0, %0, %4\n v_mul_f32 %1, %1, %4\n v_mul_f32 %2, %2, %4\n v_mul_f32 %3, %3, %4"
+                      : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3) : "v"(fb));)
+    } else if constexpr (K == 19) {
+      X4(asm volatile("v_cvt_i32_f32 %0, %4\n v_cvt_i32_f32 %1, %5\n v_cvt_i32_f32 %2, %6\n v_cvt_i32_f32 %3, %7"
+                      : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3) : "v"(f0), "v"(f1), "v"(f2), "v"(f3));
+         f0 += 1.0f;)
+    } else if constexpr (K == 20) {
+      X4(asm volatile("v_rcp_f32 %0, %0\n v_rcp_f32 %1, %1\n v_rcp_f32 %2, %2\n v_rcp_f32 %3, %3"
+                      : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));)
+    } else if constexpr (K == 21) {
+      X4(asm volatile("v_max_f32 %0, %0, %4\n v_max_f32 %1, %1, %4\n v_max_f32 %2, %2, %4\n v_max_f32 %3, %3, %4"
+                      : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3) : "v"(fb));)
+    } else if constexpr (K == 22) {
+      X4(asm volatile("v_cndmask_b32 %0, %0, %4, vcc\n v_cndmask_b32 %1, %1, %4, vcc\n v_cndmask_b32 %2, %2, %4, vcc\n v_cndmask_b32 %3, %3, %4, vcc"
+                      : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3) : "v"(b) : "vcc");)
+    } else if constexpr (K == 23) {
+      X4(asm volatile("v_add_u32 %0, %0, %4\n v_add_u32 %1, %1, %4\n v_add_u32 %2, %2, %4\n v_add_u32 %3, %3, %4"
                       : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3) : "v"(b));)
     }
   }
@@ -87,7 +119,9 @@ int main() {
   hipEventCreate(&e1);
   const char* names[] = {"v_add_f32", "v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mul_u32_u24", "v_fma_f64",
                          "v_add_f64", "v_cvt_f64_u32", "v_med3_f32", "v_pk_fma_f32", "v_cmp_f64 + 4 v_cndmask (5 insts)",
-                         "v_ldexp_f64", "v_mul_f64", "v_xor_b32", "v_mul_hi_u32_u24"};
+                         "v_ldexp_f64", "v_mul_f64", "v_xor_b32", "v_mul_hi_u32_u24", "v_fma_f32", "v_pk_add_f32",
+                         "v_pk_mul_f32", "v_mul_f32", "v_cvt_i32_f32", "v_rcp_f32", "v_max_f32", "v_cndmask_b32",
+                         "v_add_u32"};
   auto run = [&](auto k, int idx) {
     constexpr int K = decltype(k)::value;
     float best = 1e30f;
@@ -114,5 +148,14 @@ int main() {
   run(std::integral_constant<int, 10>{}, 10); run(std::integral_constant<int, 11>{}, 11);
   run(std::integral_constant<int, 12>{}, 12); run(std::integral_constant<int, 13>{}, 13);
   run(std::integral_constant<int, 14>{}, 14);
+  run(std::integral_constant<int, 15>{}, 15);
+  run(std::integral_constant<int, 16>{}, 16);
+  run(std::integral_constant<int, 17>{}, 17);
+  run(std::integral_constant<int, 18>{}, 18);
+  run(std::integral_constant<int, 19>{}, 19);
+  run(std::integral_constant<int, 20>{}, 20);
+  run(std::integral_constant<int, 21>{}, 21);
+  run(std::integral_constant<int, 22>{}, 22);
+  run(std::integral_constant<int, 23>{}, 23);
   return 0;
 }
