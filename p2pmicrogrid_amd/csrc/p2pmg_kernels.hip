@@ -1056,9 +1056,16 @@ __device__ __forceinline__ BatPre bat_pre(double soc, double cap, const BatK& b)
 // battery_rule_r<false> on a step's precomputed SoC terms (the launcher-verified domain): every
 // quotient's numerator is positive where it is used (dis: x = min(energy, avail_energy) > 0;
 // chg: x = min(-energy, avail_space) > 0 as soc < smax), so the quotients need no sign fix
+// (balance * 60) * 15 of a balance that is an f32 value: both products are exact in f64 (24 + 4 + 4
+// significant bits), and so is balance * 900 (24 + 8): one multiply, the same double
+__device__ __forceinline__ double energy_of(double balance_f32) { return balance_f32 * 900.0; }
+// -x if c else x: a sign flip of the high word (x - y == x + (-y) in IEEE arithmetic)
+__device__ __forceinline__ double neg_if(double x, bool c) {
+  return __hiloint2double(__double2hiint(x) ^ (c ? (int)0x80000000 : 0), __double2loint(x));
+}
 __device__ __forceinline__ double battery_rule_pre(double balance, double& soc, const Recip64& rcap, const BatK& b,
                                                    const BatPre& pr) {
-  const double energy = (balance * 60.0) * 15.0;
+  const double energy = energy_of(balance);
   const bool dis = balance > 0.0 && pr.avail_energy > 0.0;
   const bool chg = !dis && balance < 0.0 && !pr.full;
   const double x = dis ? (energy <= pr.avail_energy ? energy : pr.avail_energy)    // min(energy, available_energy)
@@ -1066,15 +1073,16 @@ __device__ __forceinline__ double battery_rule_pre(double balance, double& soc, 
   const double q1 = qpos64(x, rcap);     // x / capacity
   const double q2 = qpos64(x, b.r900);   // x / 900
   const double q3 = qpos64(q1, b.rse);   // (x / capacity) / sqrt(eff)
-  const double soc_n = dis ? soc - q3 : soc + b.se * q1;
-  const double bal_n = dis ? balance - q2 : balance + q2;
+  // dis: soc - q3, balance - q2; chg: soc + sqrt(eff) q1, balance + q2 -- one add each
+  const double soc_n = soc + (dis ? neg_if(q3, true) : b.se * q1);
+  const double bal_n = balance + neg_if(q2, dis);
   soc = (dis || chg) ? soc_n : soc;
   return (dis || chg) ? bal_n : balance;
 }
 template <bool CHECK = true>
 __device__ __forceinline__ double battery_rule_r(double balance, double& soc, double cap, const Recip64& rcap,
                                                  const BatK& b) {
-  const double energy = (balance * 60.0) * 15.0;
+  const double energy = energy_of(balance);  // (balance * 60) * 15, exact for the f32 balances passed in
   const double avail_energy = (fmax(0.0, soc - b.smin) * cap) * b.se;
   const double space_n = fmax(0.0, b.smax - soc) * cap;
   const double avail_space = qcore64(space_n, b.rse);
@@ -1790,7 +1798,9 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   const size_t A = (size_t)p.A;
   const KC k = scalar_constants(p);
   const Dims<true> D{k.nt, k.nT, k.nb, k.np};
-  const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
+  // the launcher sends this kernel 20^4 tables only (p2pmg_runtime.cpp, sq16 dispatch): the state
+  // count is a literal, not four kernel arguments kept in SGPRs across the loop
+  constexpr uint32_t n_states = 20u * 20u * 20u * 20u;
   const QT* __restrict__ q = reinterpret_cast<const QT*>(p.q);
   unsigned long long* const dbase = reinterpret_cast<unsigned long long*>(p.qdelta) +
                                     (size_t)(blockIdx.x % kDeltaCopies) * n_states * kQPad;
