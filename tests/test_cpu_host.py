@@ -133,3 +133,24 @@ def test_bench_helpers():
 def test_device_count_without_gpu_is_zero_or_more():
     from p2pmicrogrid_amd import _lib
     assert _lib.device_count() >= 0
+
+
+def test_battery_rule_rewrites_are_bitwise_identities():
+    """The kernels' range-free battery rule (p2pmg_kernels.hip battery_rule_pre / battery_rule_r) uses
+    two rewrites of the reference arithmetic (agent.py:138-153, storage.py:52-76; oracle
+    battery_rule): energy (b * 60) * 15 as b * 900 for an f32 balance b, and x - q as x + (-q).
+    Both are exact identities in IEEE f64; checked here over random, extreme and signed-zero f32
+    balances (the GPU parity tests compare the whole rule against the oracle bit for bit)."""
+    rs = np.random.RandomState(7)
+    f32 = np.concatenate([
+        rs.standard_normal(200000).astype(np.float32) * np.float32(5000.0),
+        (rs.standard_normal(20000) * np.exp(rs.uniform(-80, 80, 20000))).astype(np.float32),
+        np.array([0.0, -0.0, 1e-45, -1e-45, 3.4028235e38, -3.4028235e38, np.inf, -np.inf], np.float32)])
+    b = f32.astype(np.float64)
+    with np.errstate(over="ignore", invalid="ignore"):
+        two = (b * 60.0) * 15.0
+        one = b * 900.0
+    assert np.array_equal(two.view(np.int64), one.view(np.int64))
+    x = rs.standard_normal(100000) * np.exp(rs.uniform(-30, 30, 100000))
+    q = rs.standard_normal(100000) * np.exp(rs.uniform(-30, 30, 100000))
+    assert np.array_equal((x - q).view(np.int64), (x + (-q)).view(np.int64))
