@@ -358,6 +358,18 @@ __device__ __forceinline__ uint64_t code_word(const EpisodeParams& p, const Code
   return (p.mode != 0 || !active) ? ~0ull : w;
 }
 
+// the sq16 kernel's code word: its TRAIN launches are exactly p.mode == 0 (launch_sq16_nw), and a
+// masked-off lane's draws reach only its dummy stores, so no per-lane mask stays live in the loop
+template <bool TRAIN>
+__device__ __forceinline__ uint64_t code_word_t(const EpisodeParams& p, const CodeWords& c) {
+  if constexpr (!TRAIN) return ~0ull;
+  const int R1 = p.R + 1;
+  uint64_t w = (uint64_t)c.w0 | ((R1 > 4 ? (uint64_t)c.w1 : 0xFFFFFFFFull) << 32);
+  w |= (R1 < 8 ? ~0ull << (8 * R1) : 0ull);
+  if (p.rng == 1) w = c.gen;
+  return w;
+}
+
 // A TD store can hit a row whose prefetch was issued before it.  The prefetched registers
 // are not touched (that would force a wait for the load); the patch is applied at use.
 template <typename QT>
@@ -985,6 +997,11 @@ __device__ __forceinline__ Recip64 recip64(double d) {
   const double r1 = __builtin_fma(r0, __builtin_fma(-d, r0, 1.0), r0);
   return Recip64{d, __builtin_fma(r1, __builtin_fma(-d, r1, 1.0), r1), in_div_range64(d)};
 }
+// x / 900 s (storage.py) through the correctly rounded reciprocal as a compile-time constant: the
+// one Newton correction in qcore64 / qpos64 returns the IEEE quotient from it as from the device's
+// refined v_rcp_f64 estimate, and a literal is rematerialised where a kernel-argument-derived value
+// would hold two SGPRs across the loop (or spill them to VGPR lanes)
+constexpr Recip64 kR900{900.0, 1.0 / 900.0, true};
 __device__ __forceinline__ double fdiv64_ieee(double n, double d) {
   asm volatile("" : "+v"(n));
   return n / d;
@@ -1192,7 +1209,7 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   if constexpr (BAT != 0) {
     bcap = active ? p.bat_cap[a] : 0.0;
     soc = active ? p.soc[a] : 0.0;
-    bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64_u(p.bat_sqrt_eff), recip64_u(900.0)};
+    bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64_u(p.bat_sqrt_eff), kR900};
     rcap = recip64(bcap > 0.0 ? bcap : 1.0);
   }
   const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, np);  // round 0 and next state: p2p = 0 (agent.py:203)
@@ -1785,6 +1802,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   constexpr int N = 16, G = 16, SPW = kWave / G;
   __shared__ uint32_t hkey[kSqSlots];
   __shared__ unsigned long long hval[kSqSlots];
+  __shared__ double tdk[2];  // {alpha, gamma} of the TD update, read per step (see below)
   __shared__ __attribute__((aligned(16))) float tpall[kSq16Waves * SPW * kTpStride];
   const int wv = (int)(threadIdx.x / kWave);
   const int lane = (int)(threadIdx.x % kWave);
@@ -1808,6 +1826,10 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     hkey[k2] = kSqEmpty;
     hval[k2] = 0;
   }
+  if (threadIdx.x == 0) {
+    tdk[0] = p.alpha;
+    tdk[1] = p.gamma;
+  }
   __syncthreads();
   float* const tp = tpall + (wv * SPW + sl) * kTpStride;  // this scenario's tile
   // column reads of the transpose: element i of row j sits at j*16 + 4*((i>>2) ^ (j&3)) + (i&3)
@@ -1818,14 +1840,21 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   const float mi = active ? p.max_in[a] : 1.0f;
   const Recip rmi = recip(mi), rmph = recip_u(k.mph), rmargin = recip_u(k.margin);
   const float4 lv = p.hp_lv[a];
-  const bool margin_one = p.margin == 1.0f;
+  // margin == 1 (the reference's) tested per step as a scalar compare of its bits: a loop-invariant
+  // bool would be kept as a 64-bit lane mask across the loop (two SGPRs, spilled to VGPR lanes)
+  const uint32_t margin_bits = __float_as_uint(p.margin);
+  auto margin_one = [&]() __attribute__((always_inline)) {
+    uint32_t r;
+    asm volatile("s_cmp_eq_u32 %1, 0x3f800000\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(margin_bits) : "scc");
+    return r != 0;
+  };
   double bcap = 0.0, soc = 0.0;
   BatK bk{};
   Recip64 rcap{};
   if constexpr (BAT != 0) {
     bcap = p.bat_cap[a];
     soc = p.soc[a];
-    bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64_u(p.bat_sqrt_eff), recip64_u(900.0)};
+    bk = BatK{p.bat_min, p.bat_max, p.bat_sqrt_eff, recip64_u(p.bat_sqrt_eff), kR900};
     rcap = recip64(bcap > 0.0 ? bcap : 1.0);
   }
   float tin = active ? p.t_in[a] : k.setpoint;
@@ -1835,18 +1864,18 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
 
   // running element offsets in 32 bits (the launcher checks T * A * W < 2^32 and the env table
   // size): fewer 64-bit uniform values live across the loop, i.e. fewer SGPR spills
+  // (one wrapped step index, t + 2 mod T, and the offsets as scalar products of it: fewer uniform
+  // values live across the loop than three running offsets and their wrap points)
   const float* envb = p.env + (size_t)s_env * kEnvStride;
   const uint32_t env_step = (uint32_t)p.n_env * kEnvStride;
-  const uint32_t env_end = env_step * (uint32_t)T;
   const float2* profb = p.prof + a;
   const uint32_t A32 = (uint32_t)p.A;
-  const uint32_t prof_end = A32 * (uint32_t)T;
   const uint32_t* codes_a = p.codes + a;
   const uint32_t code_step = (uint32_t)W * A32;
-  auto adv = [](uint32_t off, uint32_t step, uint32_t end) { off += step; return off >= end ? off - end : off; };
-  uint32_t e1o = adv(0, env_step, env_end), e2o = adv(e1o, env_step, env_end);
-  uint32_t f1o = adv(0, A32, prof_end), f2o = adv(f1o, A32, prof_end);
-  uint32_t c1o = (T > 1) ? code_step : 0;
+  const uint32_t T32 = (uint32_t)T;
+  const uint32_t t1 = T32 > 1 ? 1u : 0u;
+  uint32_t t2 = (2u % T32);  // step t + 2 (mod T) of the loop's iteration t
+  const uint32_t e1o = t1 * env_step, f1o = t1 * A32;
   // records: FastRec rows, or only {reward, cost} as float2 when nothing else was requested
   // (8 B instead of 32 B of writes per agent-step); masked-off lanes write a dummy row.  Compile
   // time, as in the fast kernel: no store-count branch for the vmcnt bookkeeping to be pessimistic about
@@ -1866,7 +1895,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     st.bal = bal;
     st.baln = fdiv_b(fn.x - fn.y, rmi);
     const float dt = t_in - k.setpoint;
-    const float tnorm = margin_one ? dt : fdiv_b(dt, rmargin);
+    const float tnorm = margin_one() ? dt : fdiv_b(dt, rmargin);
     // rl.py:89-95 bins of the 20-state axes (the launcher sends this kernel 20^4 tables only), each
     // as one v_med3 + convert (clamp_bin_f == clamp_bin for every non-NaN value), row offsets in
     // 24-bit multiplies
@@ -1888,7 +1917,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     return gather_row(reinterpret_cast<const QT*>(qb + (row << kRowShift)));
   };
   StepIdx st = step_idx(e0.time, e1.time, fdiv_b(f0.x - f0.y, rmi), f1, tin);
-  uint64_t cw = code_word(p, step_codes(p, codes_a, 0, 0, a, W), active);
+  uint64_t cw = code_word_t<TRAIN>(p, step_codes(p, codes_a, 0, 0, a, W));
   auto row0_addr = [&](const StepIdx& x, uint64_t c) -> uint32_t {
     const bool need = ((c & 0xFF) == 255) || (TRAIN && R1 == 1);
     return need ? x.strip + (uint32_t)ip_zero : x.nrow;
@@ -1899,9 +1928,10 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   float ep_sum = 0.0f;
 
   for (int t = 0; t < T; ++t) {
-    const EnvRow e2 = load_env(envb + e2o);
-    const float2 f2 = profb[f2o];
-    const CodeWords cw1r = step_codes(p, codes_a, c1o, t + 1 == T ? 0 : t + 1, a, W);
+    const uint32_t t1n = t + 1 == T ? 0u : (uint32_t)t + 1u;  // step t + 1 (mod T)
+    const EnvRow e2 = load_env(envb + t2 * env_step);
+    const float2 f2 = profb[t2 * A32];
+    const CodeWords cw1r = step_codes(p, codes_a, t1n * code_step, (int)t1n, a, W);
     const float balw = st.bal * mi;
     float row[N];
     float col[N];
@@ -2002,7 +2032,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     float tin1 = tin, tm1 = tm;
     rc_update(k, e0.t_out, hp, tin1, tm1);
     const StepIdx st1 = step_idx(e1.time, e2.time, st.baln, f2, tin1);
-    const uint64_t cw1 = code_word(p, cw1r, active);
+    const uint64_t cw1 = code_word_t<TRAIN>(p, cw1r);
     const uint32_t a0n = row0_addr(st1, cw1);
     const Row4<QT> row0n = gatq(a0n);
     const Row4<QT> rowNn = gatq(TRAIN ? st1.nrow : a0n);
@@ -2036,7 +2066,15 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     if constexpr (TRAIN) {
       if (active) {
         const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
-        const double d = k.alpha * (((double)rw + k.gamma * (double)max3(rowN)) - (double)qsa);
+        // alpha and gamma from LDS through an address the compiler cannot hoist: a broadcast LDS
+        // read per step instead of four SGPRs held across the loop (spilled to VGPR lanes and read
+        // back with v_readlane on the VALU)
+        typedef __attribute__((address_space(3))) const double lds_double;
+        uint32_t tdk_addr = (uint32_t)(uintptr_t)(lds_double*)tdk;
+        asm volatile("" : "+s"(tdk_addr));
+        lds_double* tdp = (lds_double*)(uintptr_t)tdk_addr;
+        const double k_alpha = tdp[0], k_gamma = tdp[1];
+        const double d = k_alpha * (((double)rw + k_gamma * (double)max3(rowN)) - (double)qsa);
         const long long dv = __double2ll_rn(d * kDeltaScale);
 #if P2PMG_SQ_ABL == 1
         if (dv == 0x7123456789LL)  // timing-only ablation: no hash insert (never true in practice)
@@ -2074,9 +2112,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     e0 = e1;
     e1 = e2;
     f1 = f2;
-    e2o = adv(e2o, env_step, env_end);
-    f2o = adv(f2o, A32, prof_end);
-    c1o = (t + 2 >= T) ? 0u : c1o + code_step;
+    t2 = t2 + 1u == T32 ? 0u : t2 + 1u;
     st = st1;
     cw = cw1;
     a0 = a0n;
