@@ -574,6 +574,9 @@ def issue_roofline(workload: str, kernel_ms: float):
     valu, waves = d["counters_per_launch"]["SQ_INSTS_VALU"], d["counters_per_launch"]["SQ_WAVES"]
     achieved = valu / (kernel_ms * 1e-3) / 1e9
     out = {"unit": "G VALU wave-instructions/s", "achieved": achieved, "peak": VALU_PEAK_G,
+           # one VALU per 4 SIMD cycles: nominal, not a ceiling (gfx950 issues v_mul / v_add_f32 at
+           # 2.6 / 2.9 SIMD cycles, profiles/r04_ubench_rate.jsonl), so the fractions can pass 1
+           "peak_kind": "nominal (1 VALU / 4 SIMD cycles)",
            "frac": achieved / VALU_PEAK_G, "peak_clock_ghz": CLOCK_GHZ, "valu_insts_per_launch": valu, "waves": waves,
            "kernel": d.get("kernel"), "source": os.path.relpath(path, ROOT),
            # from the counter run itself: share of wave cycles issuing any instruction / waiting
