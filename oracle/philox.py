@@ -9,14 +9,16 @@ The reference draws exploration from the global legacy ``np.random`` MT19937 str
 SURVEY.md §3.5 (ii): one Philox block per (seed, episode, agent, t, round, tag), so the
 result is independent of how scenarios are sharded over GPUs.
 
-Block layout (must match ``p2pmicrogrid_amd/csrc/p2pmg_kernels.hip::philox_code_pair``): one
-block serves two negotiation rounds, P = ceil((R + 1) / 2) blocks per agent-step:
+Block layout (must match ``p2pmicrogrid_amd/csrc/p2pmg_device.h::philox_step_codes``): one 32-bit
+word per negotiation round, so one block serves four rounds (two agent-steps at R = 1):
     key  = (seed_lo, seed_hi)
-    ctr  = (t * P + r // 2, episode, agent_global, TAG_DECISION)
-    q    = r % 2
-    u    = x[2q] / 2**32                                      (exact in f64)
-    act  = (x[2q+1] * 3) >> 32                                (multiply-high, 3 actions)
+    k    = t * (R + 1) + r
+    ctr  = (k // 4, episode, agent_global, TAG_DECISION)
+    w    = x[k % 4]
+    u    = w / 2**32                                           (exact in f64)
     explore <=> u < epsilon   (f64 compare, as rl.py:101)
+    act  = w % 3   (used only when exploring: given u < epsilon, w is uniform on [0, thr),
+                    thr = ceil(epsilon * 2**32), so w % 3 is uniform up to 1 / thr)
 T0 draws at an episode start (tag TAG_T0, ctr = (0, episode, agent, TAG_T0)):
     Box-Muller in f64 on u1 = (x0 + 0.5) / 2**32, u2 = (x1 + 0.5) / 2**32;
     T_in = f32(setpoint + 0.3 * z0), T_m = f32(setpoint + 0.3 * z1)   (heating.py:149-152)
@@ -31,7 +33,7 @@ W0 = np.uint64(0x9E3779B9)
 W1 = np.uint64(0xBB67AE85)
 MASK32 = np.uint64(0xFFFFFFFF)
 
-TAG_DECISION = 0x5EED0003  # two rounds per block (0x5EED0001 was one block per round)
+TAG_DECISION = 0x5EED0004  # one word per round, four rounds per block (0x5EED0003: two rounds per block)
 TAG_T0 = 0x5EED0002
 
 
@@ -62,11 +64,11 @@ def decision_draws(seed: int, episode: int, agents, t: int, r: int, rounds: int)
     agents = np.asarray(agents, dtype=np.uint64)
     k0 = seed & 0xFFFFFFFF
     k1 = (seed >> 32) & 0xFFFFFFFF
-    pairs = (rounds + 2) // 2
-    x = philox4x32_10(t * pairs + r // 2, episode, agents, TAG_DECISION, k0, k1)
-    q = r % 2
-    u = x[2 * q].astype(np.float64) / 4294967296.0
-    act = ((x[2 * q + 1] * np.uint64(3)) >> np.uint64(32)).astype(np.int64)
+    k = t * (rounds + 1) + r
+    x = philox4x32_10(k // 4, episode, agents, TAG_DECISION, k0, k1)
+    w = x[k % 4]
+    u = w.astype(np.float64) / 4294967296.0
+    act = (w % np.uint64(3)).astype(np.int64)
     return u, act
 
 

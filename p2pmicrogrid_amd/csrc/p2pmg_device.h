@@ -55,8 +55,43 @@ __device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32
     c3 = lo0;
   }
 }
-constexpr uint32_t kTagDecision = 0x5EED0003u;  // one block per two rounds (oracle/philox.py)
+constexpr uint32_t kTagDecision = 0x5EED0004u;  // one 32-bit word per round (oracle/philox.py)
 constexpr uint32_t kTagT0 = 0x5EED0002u;
+
+// Philox exploration stream (oracle/philox.py::decision_draws; QActor.select_action rl.py:100-111):
+// round r of step t of agent gid uses word k % 4 of the block ctr = (k / 4, episode, gid,
+// kTagDecision), k = t (R + 1) + r.  The agent explores when w / 2^32 < eps (w < thr, eps_threshold)
+// and then takes action w % 3: given w < thr, w is uniform on [0, thr), so w % 3 is uniform up to
+// 1 / thr.  One word per round: a block serves four rounds (two steps at R = 1).  255 = greedy.
+__device__ __forceinline__ uint32_t decision_code(uint32_t w, uint32_t thr, int all) {
+  return (all || w < thr) ? w % 3u : 255u;
+}
+// the four codes of block blk, byte j = word j
+__device__ __forceinline__ uint32_t philox_block_codes(uint32_t blk, uint32_t episode, uint32_t gid, uint32_t thr,
+                                                       int all, uint32_t k0, uint32_t k1) {
+  uint32_t c0 = blk, c1 = episode, c2 = gid, c3 = kTagDecision;
+  // the round keys derive from the seed afresh in each call (SALU adds): hoisted out of an episode
+  // loop they would be 20 uniform values held across it
+  asm volatile("" : "+s"(k0), "+s"(k1));
+  philox4x32_10(c0, c1, c2, c3, k0, k1);
+  return decision_code(c0, thr, all) | (decision_code(c1, thr, all) << 8) | (decision_code(c2, thr, all) << 16) |
+         (decision_code(c3, thr, all) << 24);
+}
+// every round's code of step t, byte r (bytes r >= R1: 255); R1 <= 8
+__device__ __forceinline__ uint64_t philox_step_codes(int t, int R1, uint32_t episode, uint32_t gid, uint32_t thr,
+                                                      int all, uint32_t k0, uint32_t k1) {
+  const uint32_t kf = (uint32_t)t * (uint32_t)R1, kl = kf + (uint32_t)R1 - 1u;
+  uint64_t out = ~0ull;
+  for (uint32_t b = kf >> 2; b <= (kl >> 2); ++b) {
+    const uint32_t c4 = philox_block_codes(b, episode, gid, thr, all, k0, k1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = (int)(4u * b + (uint32_t)j) - (int)kf;
+      if (r >= 0 && r < R1) out = (out & ~(0xFFull << (8 * r))) | ((uint64_t)((c4 >> (8 * j)) & 0xFFu) << (8 * r));
+    }
+  }
+  return out;
+}
 
 // RuleAgent._update_storage (agent.py:138-153) with BatteryStorage bookkeeping (storage.py:79-100),
 // f64 like the reference's Python floats.  Returns the adjusted balance (W); soc is updated.

@@ -172,12 +172,10 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
       if (p.rng == 0) {
         code = (int)((p.codes[((size_t)t * W + (r >> 2)) * A + a] >> (8 * (r & 3))) & 0xFFu);
       } else {
-        // one Philox block per two rounds (oracle/philox.py::decision_draws)
-        uint32_t c0 = (uint32_t)(t * ((R1 + 1) >> 1) + (r >> 1)), c1 = (uint32_t)p.episode,
-                 c2 = p.agent_offset + (uint32_t)a, c3 = kTagDecision;
-        philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-        const uint32_t wu = (r & 1) ? c2 : c0, wa = (r & 1) ? c3 : c1;
-        code = (p.eps_all || wu < p.eps_thr) ? (int)__umulhi(wa, 3u) : 255;  // wu / 2^32 < eps
+        // word k = t (R + 1) + r of the agent's decision stream (p2pmg_device.h, oracle/philox.py::decision_draws)
+        const uint32_t k = (uint32_t)t * (uint32_t)R1 + (uint32_t)r;
+        code = (int)((philox_block_codes(k >> 2, (uint32_t)p.episode, p.agent_offset + (uint32_t)a, p.eps_thr, p.eps_all,
+                                         p.seed_lo, p.seed_hi) >> (8 * (k & 3u))) & 0xFFu);
       }
     }
     if (code == 255) {
@@ -419,14 +417,9 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
         codes_pack = (codes_pack & ~(0xFFFFFFFFull << (32 * w4))) |
                      ((uint64_t)p.codes[((size_t)t * W + w4) * A + a] << (32 * w4));
     } else {
-      for (int q = 0; 2 * q < R1; ++q) {  // one Philox block per two rounds (oracle/philox.py::decision_draws)
-        uint32_t c0 = (uint32_t)(t * ((R1 + 1) >> 1) + q), c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a,
-                 c3 = kTagDecision;
-        philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-        const uint64_t k0 = (p.eps_all || c0 < p.eps_thr) ? __umulhi(c1, 3u) : 255u;  // c0 / 2^32 < eps
-        const uint64_t k1 = (p.eps_all || c2 < p.eps_thr) ? __umulhi(c3, 3u) : 255u;
-        codes_pack = (codes_pack & ~(0xFFFFull << (16 * q))) | (k0 << (16 * q)) | (k1 << (16 * q + 8));
-      }
+      // every round's code of step t (p2pmg_device.h, oracle/philox.py::decision_draws)
+      codes_pack = philox_step_codes(t, R1, (uint32_t)p.episode, p.agent_offset + (uint32_t)a, p.eps_thr, p.eps_all,
+                                     p.seed_lo, p.seed_hi);
     }
   }
   const int tag4 = reduce4_tag();

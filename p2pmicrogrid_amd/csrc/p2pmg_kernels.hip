@@ -311,20 +311,11 @@ __device__ __forceinline__ StepIdx make_step(const KC& p, const Dims<B20>& D, bo
   return st;
 }
 
-// Philox exploration draws of rounds 2 pair and 2 pair + 1 at step t from ONE block: code of
-// round 2 pair in bits 0..7, of round 2 pair + 1 in bits 8..15; 255 = greedy
-// (QActor.select_action rl.py:100-111).  Layout: oracle/philox.py::decision_draws.
-__device__ __forceinline__ uint32_t philox_code_pair(const EpisodeParams& p, int t, int pair, uint32_t gid) {
-  const int pairs = (p.R + 2) >> 1;
-  uint32_t c0 = (uint32_t)(t * pairs + pair), c1 = (uint32_t)p.episode, c2 = gid, c3 = kTagDecision;
-  philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
-  const uint32_t a0 = (uint32_t)(((uint64_t)c1 * 3ull) >> 32), a1 = (uint32_t)(((uint64_t)c3 * 3ull) >> 32);
-  const uint32_t k0 = (p.eps_all || c0 < p.eps_thr) ? a0 : 255u;  // c0 / 2^32 < eps
-  const uint32_t k1 = (p.eps_all || c2 < p.eps_thr) ? a1 : 255u;
-  return k0 | (k1 << 8);
-}
-__device__ __forceinline__ uint32_t philox_code(const EpisodeParams& p, int t, int r, uint32_t gid) {
-  return (philox_code_pair(p, t, r >> 1, gid) >> (8 * (r & 1))) & 0xFFu;
+// Philox exploration codes of every round of step t (p2pmg_device.h::philox_step_codes, layout
+// oracle/philox.py::decision_draws): byte r = code of round r, 255 = greedy (QActor.select_action
+// rl.py:100-111)
+__device__ __forceinline__ uint64_t philox_codes_of(const EpisodeParams& p, int t, uint32_t gid) {
+  return philox_step_codes(t, p.R + 1, (uint32_t)p.episode, gid, p.eps_thr, p.eps_all, p.seed_lo, p.seed_hi);
 }
 
 // all rounds' codes of step t packed one byte per round (round r in bits 8r..8r+7)
@@ -336,18 +327,13 @@ struct CodeWords {
   uint64_t gen;     // in-kernel Philox word (p.rng == 1)
 };
 __device__ __forceinline__ CodeWords step_codes(const EpisodeParams& p, const uint32_t* codes_a, size_t off, int t,
-                                                int a, int W) {
+                                                int a, int W, bool gen = true) {
   // code words [T][W][A] (replay upload or Philox pre-pass); off = t * W * A
   CodeWords c;
   c.w0 = codes_a[off];
   c.w1 = codes_a[W > 1 ? off + (size_t)p.A : off];
   c.gen = ~0ull;
-  if (p.rng == 1) {
-    for (int r = 0; r <= p.R; r += 2) {
-      const uint64_t v = philox_code_pair(p, t, r >> 1, p.agent_offset + (uint32_t)a);
-      c.gen = (c.gen & ~(0xFFFFull << (8 * r))) | (v << (8 * r));
-    }
-  }
+  if (gen && p.rng == 1) c.gen = philox_codes_of(p, t, p.agent_offset + (uint32_t)a);
   return c;
 }
 __device__ __forceinline__ uint64_t code_word(const EpisodeParams& p, const CodeWords& c, bool active) {
@@ -799,15 +785,8 @@ __global__ void philox_codes_kernel(const EpisodeParams p, uint32_t* __restrict_
   if (k >= (size_t)p.T * p.A) return;
   const int t = (int)(k / p.A), a = (int)(k % p.A);
   const int R1 = p.R + 1, W = (R1 + 3) >> 2;
-  for (int w = 0; w < W; ++w) {
-    uint32_t word = 0xFFFFFFFFu;
-    for (int b = 0; b < 4 && 4 * w + b < R1; b += 2) {
-      uint32_t c = philox_code_pair(p, t, (4 * w + b) >> 1, p.agent_offset + (uint32_t)a);
-      if (4 * w + b + 1 >= R1) c |= 0xFF00u;
-      word = (word & ~(0xFFFFu << (8 * b))) | (c << (8 * b));
-    }
-    words[((size_t)t * W + w) * p.A + a] = word;
-  }
+  const uint64_t codes = philox_codes_of(p, t, p.agent_offset + (uint32_t)a);
+  for (int w = 0; w < W; ++w) words[((size_t)t * W + w) * p.A + a] = (uint32_t)(codes >> (32 * w));
 }
 #endif
 
@@ -948,15 +927,8 @@ __device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOu
     q.eps_thr = o.eps_thr;
     q.eps_all = o.eps_all;
     const int R1 = p.R + 1, W = (R1 + 3) >> 2;
-    for (int w = 0; w < W; ++w) {
-      uint32_t word = 0xFFFFFFFFu;
-      for (int b = 0; b < 4 && 4 * w + b < R1; b += 2) {
-        uint32_t c = philox_code_pair(q, t, (4 * w + b) >> 1, p.agent_offset + (uint32_t)a);
-        if (4 * w + b + 1 >= R1) c |= 0xFF00u;
-        word = (word & ~(0xFFFFu << (8 * b))) | (c << (8 * b));
-      }
-      o.words[((size_t)t * W + w) * p.A + a] = word;
-    }
+    const uint64_t codes = philox_codes_of(q, t, p.agent_offset + (uint32_t)a);
+    for (int w = 0; w < W; ++w) o.words[((size_t)t * W + w) * p.A + a] = (uint32_t)(codes >> (32 * w));
   }
 }
 #if P2PMG_IN_PART(0)
@@ -1917,7 +1889,17 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     return gather_row(reinterpret_cast<const QT*>(qb + (row << kRowShift)));
   };
   StepIdx st = step_idx(e0.time, e1.time, fdiv_b(f0.x - f0.y, rmi), f1, tin);
-  uint64_t cw = code_word_t<TRAIN>(p, step_codes(p, codes_a, 0, 0, a, W));
+  // R + 1 = 2 in-kernel Philox: one block holds the codes of two steps (p2pmg_device.h), computed
+  // at the even step and kept for the odd one in the code word's unused high half
+  constexpr bool kPair = R1 == 2 && TRAIN;
+  const bool rng1 = p.rng == 1;
+  auto block2 = [&](uint32_t blk) -> uint64_t {
+    const uint32_t c4 = philox_block_codes(blk, (uint32_t)p.episode, p.agent_offset + (uint32_t)a, p.eps_thr, p.eps_all,
+                                           p.seed_lo, p.seed_hi);
+    return (uint64_t)(c4 & 0xFFFFu) | ((uint64_t)(c4 >> 16) << 32) | 0xFFFF0000FFFF0000ull;
+  };
+  uint64_t cw = code_word_t<TRAIN>(p, step_codes(p, codes_a, 0, 0, a, W, !kPair));
+  if (kPair && rng1) cw = block2(0);
   auto row0_addr = [&](const StepIdx& x, uint64_t c) -> uint32_t {
     const bool need = ((c & 0xFF) == 255) || (TRAIN && R1 == 1);
     return need ? x.strip + (uint32_t)ip_zero : x.nrow;
@@ -1931,7 +1913,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     const uint32_t t1n = t + 1 == T ? 0u : (uint32_t)t + 1u;  // step t + 1 (mod T)
     const EnvRow e2 = load_env(envb + t2 * env_step);
     const float2 f2 = profb[t2 * A32];
-    const CodeWords cw1r = step_codes(p, codes_a, t1n * code_step, (int)t1n, a, W);
+    const CodeWords cw1r = step_codes(p, codes_a, t1n * code_step, (int)t1n, a, W, !kPair);
     const float balw = st.bal * mi;
     float row[N];
     float col[N];
@@ -2032,7 +2014,10 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     float tin1 = tin, tm1 = tm;
     rc_update(k, e0.t_out, hp, tin1, tm1);
     const StepIdx st1 = step_idx(e1.time, e2.time, st.baln, f2, tin1);
-    const uint64_t cw1 = code_word_t<TRAIN>(p, cw1r);
+    uint64_t cw1 = code_word_t<TRAIN>(p, cw1r);
+    if constexpr (kPair) {
+      if (rng1) cw1 = (t1n & 1u) ? ((cw >> 32) | 0xFFFFFFFF00000000ull) : block2(t1n >> 1);
+    }
     const uint32_t a0n = row0_addr(st1, cw1);
     const Row4<QT> row0n = gatq(a0n);
     const Row4<QT> rowNn = gatq(TRAIN ? st1.nrow : a0n);

@@ -29,6 +29,14 @@ def test_philox_draws_are_uniform_and_deterministic():
     assert np.array_equal(u, u2) and np.array_equal(a, a2)
     assert 0.49 < u.mean() < 0.51 and set(np.unique(a)) == {0, 1, 2}
     assert abs((a == 0).mean() - 1 / 3) < 0.01
+    # one word per round: the action of an exploring draw (u < eps) is w % 3 of the same word, uniform
+    # over the three actions for any epsilon, and the four rounds of a block are distinct words
+    for eps in (0.1, 0.5, 0.81):
+        ex = u < eps
+        for k in range(3):
+            assert abs((a[ex] == k).mean() - 1 / 3) < 0.02
+    w = [philox.decision_draws(42, 3, np.arange(1000), t, r, 1)[0] for t in (4, 5) for r in (0, 1)]
+    assert len({tuple(x[:8]) for x in w}) == 4
     ti, tm = philox.t0_draws(42, 0, np.arange(20000))
     assert abs(ti.mean() - 21.0) < 0.01 and abs(ti.std() - 0.3) < 0.01 and abs(tm.std() - 0.3) < 0.01
 
