@@ -756,17 +756,11 @@ __device__ __forceinline__ void load_train_w(TrainW& W, const float* th, const f
 #ifndef P2PMG_TRAIN_OCC
 #define P2PMG_TRAIN_OCC 2
 #endif
-#ifndef P2PMG_TRAIN_NOB4
-#define P2PMG_TRAIN_NOB4 0
-#endif
-constexpr bool kTrainNoB4 = P2PMG_TRAIN_NOB4;
 template <bool SHARED>
 __global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const DqnParams d) {
   __shared__ float smpb[2][kB * kTrans];  // this agent's batch and the next one's (prefetched)
   __shared__ float H1t[3 * kB][kLdsRow];
-  // online layer-1 activations, unit-major; NOB4: double-buffered by agent parity, so the next
-  // agent's layer 1 may write while a slower wave still reads this agent's in its backward
-  __shared__ __attribute__((aligned(16))) float H1oTb[kTrainNoB4 ? 2 : 1][kH][kLdsRowT];
+  __shared__ __attribute__((aligned(16))) float H1oT[kH][kLdsRowT];  // online layer-1 activations, unit-major
   __shared__ __attribute__((aligned(16))) float dZ2[kB][kLdsRow];
   __shared__ float qpart[4][4 * kB];  // per-wave partial Q: rows 0..95 target (action x sample), 96..127 online
   const EpisodeParams& p = d.e;
@@ -832,7 +826,6 @@ __global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const D
     const float* tg = d.target + (size_t)net * kNetStride;
     if (!SHARED) load_train_w(W, th, tg, col, g4, h0);
     float (*smp)[kTrans] = reinterpret_cast<float (*)[kTrans]>(smpb[ag & 1]);
-    float (*const H1oT)[kLdsRowT] = H1oTb[kTrainNoB4 ? (ag & 1) : 0];
     // prefetch the next agent's batch into registers; it goes to the other buffer at the end
     const bool has_next = !d.batch && ag + 1 < n_ag;
     float nx0, nx1;
@@ -902,10 +895,6 @@ __global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const D
       ao[1] = mfma4(bo, H1oT[k][16 + c16], ao[1]);
     }
     __builtin_amdgcn_s_setprio(0);
-    // NOB4: the next agent's batch into the other buffer here: after this agent's first barrier every
-    // wave has finished the previous agent (that buffer's last reader), and every write lands before
-    // the second barrier, which the next agent's layer-1 reads follow
-    if (kTrainNoB4 && has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
     DQN_STAMP(2);
     // ---- layer 3, this wave's 16 units: in-lane over r (a pairwise tree), then over the 4 row
     // groups for four tiles at once (reduce4_groups: 3 lane swaps + 3 adds, row group g4 ends with
@@ -1050,12 +1039,9 @@ __global__ __launch_bounds__(256, P2PMG_TRAIN_OCC) void dqn_train_kernel(const D
         for (int k = 0; k < 5; ++k) gx1[k] = fmaf(xr[k], dz1, gx1[k]);
       }
     __builtin_amdgcn_s_setprio(0);
-    if (!kTrainNoB4 && has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
+    if (has_next) batch_put(smpb[(ag + 1) & 1], threadIdx.x, nx0, nx1);
     DQN_STAMP(5);
-    // NOB4: no end-of-agent barrier: the next agent's first LDS writes (H1t, the other H1oT buffer)
-    // are not read by this agent's backward, and its later ones (qpart, dZ2) follow its own first
-    // barrier, which every wave reaches only after finishing this agent
-    if (!kTrainNoB4) __syncthreads();  // every wave is done with this agent's LDS
+    __syncthreads();  // every wave is done with this agent's LDS and with the online W2
     DQN_STAMP(1);
   }
 #if P2PMG_TRACE
