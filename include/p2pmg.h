@@ -59,7 +59,9 @@ typedef struct p2pmg_ctx p2pmg_ctx;
 #define P2PMG_MODE_FILL 2   /* DQN init_buffers (community.py:125-147): act + store memory, no training */
 
 #define P2PMG_RNG_REPLAY 0 /* exploration codes supplied by the host (reference stream) */
-#define P2PMG_RNG_PHILOX 1 /* counter-keyed Philox4x32-10 on (seed, episode, agent, t, round) */
+#define P2PMG_RNG_PHILOX 1 /* counter-keyed Philox4x32-10 on (seed, episode, agent, t, round): one 32-bit
+                              word per round, explore if w / 2^32 < epsilon, action w % 3 (round-4
+                              layout, oracle/philox.py::decision_draws) */
 
 /* per-step records (bit mask for p2pmg_episode_args.record and p2pmg_get_record) */
 #define P2PMG_REC_REWARD 1   /* f32 [T][A] reward (agent.py:225-232) */
