@@ -330,14 +330,25 @@ def _cpu_worker(job):
     return globals()[name](**kw)
 
 
-def cpu_workers() -> int:
-    """Host cores the CPU baseline may use: this process's CPU affinity, capped at 16 (a GPU box's
-    CPU share per GPU; os.cpu_count() there reports the whole machine)."""
+def cpu_workers():
+    """(workers, rule): host cores the CPU baseline may use = one GPU's share of the box.  A GPU box
+    gives each GPU 16 host cores and says so in OMP_NUM_THREADS (= MAX_JOBS = 16 there), while
+    os.cpu_count() reports the whole machine; so the share is OMP_NUM_THREADS when it is set, else
+    os.cpu_count() // the GPUs the node exposes (all cores without a GPU), never more than this
+    process's CPU affinity.  P2PMG_CPU_WORKERS overrides."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        n = os.cpu_count() or 1
-    return max(1, min(16, n, int(os.environ.get("P2PMG_CPU_WORKERS", "16"))))
+        aff = os.cpu_count() or 1
+    if os.environ.get("P2PMG_CPU_WORKERS"):
+        n, rule = int(os.environ["P2PMG_CPU_WORKERS"]), "P2PMG_CPU_WORKERS"
+    elif os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        n, rule = int(os.environ["OMP_NUM_THREADS"]), "OMP_NUM_THREADS (the box's per-GPU CPU share)"
+    else:
+        g = visible_gpus()
+        n, rule = (os.cpu_count() or 1) // max(1, g), f"os.cpu_count() // {max(1, g)} visible GPU(s)"
+    n = max(1, min(n, aff))
+    return n, f"{rule}, capped by the CPU affinity ({aff})"
 
 
 def cpu_baseline_all_cores(name: str, kw: dict, workers: int) -> dict:
@@ -473,9 +484,10 @@ def main_dqn(args, rank, world, local, S, N, R, T):
         if coll and xk != "host":
             out["collective"] = coll
         if world == 1 and not args.no_cpu_baseline:
+            workers, rule = cpu_workers()
             out["cpu_baseline"] = cpu_baseline_all_cores("cpu_baseline_dqn", dict(seconds=args.cpu_seconds, R=R, T=T),
-                                                         cpu_workers())
-            out["cpu_baseline"].update(os_cpu_count=os.cpu_count())
+                                                         workers)
+            out["cpu_baseline"].update(os_cpu_count=os.cpu_count(), cores_rule=rule)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
@@ -641,6 +653,244 @@ def load_traffic(path: str, workload: str):
     return d
 
 
+REFERENCE_EPISODES = 1000  # setup.py:30 max_episodes: the reference's training run (community.py:272-298)
+
+
+def timed(eng, world, fn):
+    """Run fn() between a barrier + device sync on both sides; the MAX of every rank's wall time."""
+    eng.sync()
+    barrier(world)
+    eng.sync()
+    t0 = time.perf_counter()
+    fn()
+    eng.sync()
+    barrier(world)
+    rank_times = all_gather_float(time.perf_counter() - t0, world)
+    return max(rank_times), rank_times
+
+
+def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None, q_dtype=None, steps=20,
+                warmup=5, cpu_seconds=10.0, schedule_to=0, eps_windows=(), window_steps=20):
+    """One tabular workload (configs[1], [2] or [3]) on this rank: build the context, run `warmup`
+    untimed then `steps` timed training episodes, and (rank 0) return its bench record; other ranks
+    return None.  schedule_to > 0 (per-agent tables): the same context then continues the
+    reference's epsilon schedule up to that episode (community.py:272-298), timing `window_steps`
+    episodes from each start in eps_windows and the whole continuation (value_at_eps)."""
+    from p2pmicrogrid_amd.dataset import apply_asset_mix, asset_mix, scenario_batch
+    DeviceCommunityBatch = engine_class()
+    S0, N0, R0, T0, qd0, shared, battery = WORKLOADS[wl]
+    hetero = wl in HETERO
+    S, N, T, q_dtype = S or S0, N or N0, T or T0, q_dtype or qd0
+    R = R0 if R is None else R
+    first = rank * S
+    inp = scenario_batch(S, N, T, first_scenario=first)
+    mix = None
+    if hetero:
+        mix = asset_mix(S, N, first_scenario=first, battery_j=BATTERY_J)
+        inp = apply_asset_mix(inp, mix)
+    eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=local, scenario_offset=first, shared_q=shared)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    del inp
+    if mix is not None:
+        eng.set_hp_levels(mix.hp_levels)
+        eng.set_battery(mix.battery_capacity)
+    elif battery:
+        eng.set_battery(BATTERY_J)
+    # episode metrics (+ the shared table's per-episode delta all-reduce, which needs RCCL)
+    xk = exchange_kind(args, world)
+    fallback = None
+    if xk == "host":  # rehearsal: int64 deltas and metrics summed over gloo
+        comm_err = "host-rehearsal exchange (no RCCL communicator)"
+    else:
+        comm_err = rccl_comm(eng, rank, world, required=shared and args.exchange == "rccl")
+        if comm_err and shared:  # --exchange auto without a communicator: the labelled host exchange
+            fallback, xk = comm_err, "host"
+    record = ("reward", "cost")
+    metrics = [None]
+
+    def episode(e):
+        if shared:
+            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record,
+                            next_epsilon=epsilon_at(e + 1))
+            if world > 1 and xk == "host":
+                from p2pmicrogrid_amd.distributed import all_reduce_int64
+                eng.set_q_delta(all_reduce_int64(eng.get_q_delta(), world))
+            elif world > 1:
+                eng.allreduce_q_delta()
+            eng.apply_q_delta()
+            eng.reset_temperatures_philox(e + 1, 0.3)  # agent.reset() at the end of train_episode
+        else:  # the same reset, fused into the episode launch
+            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record, reset_sigma=0.3,
+                            next_epsilon=epsilon_at(e + 1))
+
+    def episodes(e0, e1):
+        for k, e in enumerate(range(e0, e1)):
+            episode(e)
+            if (k + 1) % args.metric_every == 0 or e + 1 == e1:
+                metrics[0] = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
+
+    for e in range(warmup):
+        episode(e)
+    eng.sync()
+    eng.reset_kernel_times()
+    # HIP events on every launch cost ~4 us per configs[1] episode: sample every 5th launch
+    timing_period = 5 if steps >= 20 else 1
+    eng.set_timing_period(timing_period)
+    dt, rank_times = timed(eng, world, lambda: episodes(warmup, warmup + steps))
+    kms = eng.kernel_times()
+    coll = collective_record(eng, world, steps)
+    ep_reward = metrics[0][0] / metrics[0][1]
+    nranks = eng.comm_nranks() if not comm_err else 0
+    if shared and xk == "host":  # every replica's fingerprint, gathered over gloo
+        from p2pmicrogrid_amd.distributed import all_gather_concat
+        hashes = all_gather_concat(eng.table_hash_allgather().astype(np.uint64), world)
+    else:
+        hashes = eng.table_hash_allgather() if shared else None  # every replica of the shared table
+    steps_per_episode = S * N * T
+
+    # the rest of the reference's schedule on the same context: epsilon windows + the whole continuation
+    at_eps = None
+    if schedule_to and not shared and schedule_to > warmup + steps:
+        at_eps = {"episodes_total": schedule_to, "windows": []}
+        cur = warmup + steps
+        t_all = 0.0
+        for w0 in sorted(w for w in eps_windows if cur <= w and w + window_steps <= schedule_to):
+            dt_gap, _ = timed(eng, world, lambda: episodes(cur, w0))
+            eng.reset_kernel_times()
+            dt_w, _ = timed(eng, world, lambda: episodes(w0, w0 + window_steps))
+            kw_ = eng.kernel_times()
+            at_eps["windows"].append({
+                "first_episode": w0, "episodes": window_steps, "epsilon": epsilon_at(w0),
+                "epsilon_last": epsilon_at(w0 + window_steps - 1),
+                "value": world * steps_per_episode * window_steps / dt_w, "ms_per_step": dt_w / window_steps * 1e3,
+                "kernel_ms": float(np.mean(kw_)) if len(kw_) else None, "timed_launches": int(len(kw_))})
+            t_all += dt_gap + dt_w
+            cur = w0 + window_steps
+        dt_tail, _ = timed(eng, world, lambda: episodes(cur, schedule_to))
+        t_all += dt_tail
+        n_cont = schedule_to - (warmup + steps)
+        at_eps["continuation"] = {
+            "first_episode": warmup + steps, "episodes": n_cont,
+            "epsilon_range": [epsilon_at(warmup + steps), epsilon_at(schedule_to - 1)],
+            "value": world * steps_per_episode * n_cont / t_all, "ms_per_step": t_all / n_cont * 1e3,
+            "note": "wall time of every episode after the timed region up to the reference's max_episodes "
+                    "(setup.py:30), metric all-reduce every --metric-every episodes, max over ranks"}
+        at_eps["mean_episode_reward_last"] = metrics[0][0] / metrics[0][1]
+
+    out = None
+    if rank == 0:
+        value = world * steps_per_episode * steps / dt
+        q_bytes = 8 if q_dtype == "f64" else 4
+        if shared:
+            bpa = algorithmic_bytes_per_agent_step_shared(S * N, q_bytes, battery, outputs=len(record))
+            workload = (f"configs[2]: {S} scenarios/GPU x {N} agents (R={R}, T={T}) with battery storage, one "
+                        f"shared {q_dtype} Q-table, int64 delta all-reduce per episode, Philox exploration, "
+                        f"train episodes")
+        elif hetero:
+            bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
+            workload = (f"configs[3]: {S} scenarios/GPU x {N} heterogeneous households (R={R}, T={T} = "
+                        f"{T // 96} days; no-PV / heat-pump size / battery mixes), per-agent {q_dtype} Q-tables, "
+                        f"Philox exploration, train episodes")
+        else:
+            bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
+            workload = (f"configs[1]: {S} scenarios/GPU x thesis community (N={N}, R={R}, T={T}), per-agent "
+                        f"{q_dtype} Q-tables, Philox exploration, train episodes")
+        kernel_ms = float(np.mean(kms)) if len(kms) else float("nan")
+        achieved = bpa * steps_per_episode / (kernel_ms * 1e-3) / 1e9
+        tj = args.traffic_json if (args.traffic_json and wl == args.workload) else os.path.join(
+            ROOT, "profiles", "pmc_traffic.json" if wl == "config2" else f"pmc_traffic_{wl}.json")
+        traffic = load_traffic(tj, workload)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": warmup,
+            "ms_per_step": dt / steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 simulation, f64 Q-table" if q_dtype == "f64" else "f32",
+            "data": "synthetic profiles with the reference dataset schema (seed 42)",
+            "config": {"workload": workload, "scenarios_per_gpu": S, "agents_per_scenario": N,
+                       "rounds": R, "negotiation_rounds": R + 1, "horizon": T, "q_dtype": q_dtype, "shared_q": shared,
+                       "battery": battery, "agent_steps_per_step": world * steps_per_episode,
+                       "parallelism": (f"scenario-sharded x{world}, shared-table delta all-reduce (RCCL)" if shared
+                                       else f"scenario-sharded x{world} (replicas, no data-path collective)")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
+                         "kernel": eng.last_kernel(),
+                         "kernel_ms": kernel_ms,
+                         "algorithmic_bytes_per_agent_step": bpa,
+                         "algorithmic_bytes_per_launch": bpa * steps_per_episode,
+                         "timed_launches": int(len(kms)), "timing_period": timing_period},
+            "mean_episode_reward": ep_reward,
+            "epsilon_range": [epsilon_at(warmup), epsilon_at(warmup + steps - 1)],
+            "rccl_nranks": nranks,
+            "rank_times_s": rank_times,
+        }
+        if os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
+            out["test_engine"] = os.environ["P2PMG_BENCH_TEST_ENGINE"]
+        if comm_err:
+            out["rccl_error"] = comm_err
+        if world > 1:
+            out["exchange"] = "host-rehearsal" if xk == "host" else "rccl"
+        if fallback:
+            out["exchange_fallback"] = f"RCCL unavailable ({fallback}): int64 deltas summed over gloo"
+        if coll and xk != "host":
+            out["collective"] = coll
+        if shared:
+            out["table_replicas_identical"] = bool(np.all(hashes == hashes[0]))
+            assert out["table_replicas_identical"], f"shared-table replicas differ across ranks: {hashes}"
+        if traffic:
+            out["roofline"]["traffic_source"] = traffic.get("source")
+        if not shared and q_dtype == "f64" and N <= 8:  # the fast kernel's sector-granular traffic model
+            eps_mid = epsilon_at(warmup + steps // 2)
+            sm = sector_model_per_agent_step(N, R, eps_mid, battery or hetero)
+            sm["bytes_per_launch"] = sm["total"] * steps_per_episode
+            out["roofline"]["sector_model"] = sm
+        issue = issue_roofline(wl, kernel_ms)
+        if issue:
+            out["roofline"]["issue"] = issue
+        # What binds the kernel (DESIGN.md §5): achieved/peak/frac above stay the HBM roofline
+        # (algorithmic bytes); "bound" names the limit the measurements point to and
+        # "binding_frac" is the fraction against that limit.
+        if not (shared or battery or hetero) and q_dtype == "f64" and N == 2 and R == 1:
+            gather = gather_roofline(S * N, T, kernel_ms)
+            if gather:
+                out["roofline"]["gather_floor"] = gather
+                out["roofline"]["bound"] = "latency"  # one wave per CU: the dependent row-gather chain
+                out["roofline"]["binding_frac"] = gather["frac"]
+        elif hetero and q_dtype == "f64" and N == 4 and R == 1:
+            gather = gather_roofline(S * N, T, kernel_ms, stages=2, agents_per_wave=64, pool=400, rows=3,
+                                     source="r04_ubench_gather.jsonl")
+            if gather:  # two dependent gather round trips per step + the f64 battery rules on the chain
+                out["roofline"]["gather_floor"] = gather
+                out["roofline"]["bound"] = "latency"
+                out["roofline"]["binding_frac"] = gather["frac"]
+        elif shared and issue and issue["frac"] > 0.5:
+            out["roofline"]["bound"] = "valu-issue"  # every SIMD busy: VALU instructions per agent-step
+            out["roofline"]["binding_frac"] = issue["frac"]
+        if at_eps:
+            out["value_at_eps"] = at_eps
+    eng.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_seconds > 0:
+        workers, rule = cpu_workers()
+        cb = cpu_baseline_all_cores("cpu_baseline", dict(
+            seconds=cpu_seconds, S=(64 if hetero else 256) if N <= 4 else 64, N=N, R=R, T=T, q_dtype=q_dtype,
+            shared=shared, battery=battery, hetero=hetero, t_sample=960 if T > 960 else 0), workers)
+        cb.update(os_cpu_count=os.cpu_count(), cores_rule=rule)
+        if not (shared or battery or hetero):  # the per-object loop restates the tabular path only
+            cb["per_object"] = cpu_baseline_per_object(min(cpu_seconds, 5.0), N=N, R=R, T=T)
+        out["cpu_baseline"] = cb
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=None,
@@ -664,6 +914,22 @@ def main():
                          "host (gloo rehearsal; auto picks it only when the launcher maps ranks onto shared GPUs)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary for roofline.traffic (default profiles/pmc_traffic[_<workload>].json)")
+    ap.add_argument("--schedule-episodes", type=int, default=None,
+                    help="per-agent tables: continue the same context through the reference's epsilon schedule up "
+                         f"to this episode and time it (value_at_eps; default {REFERENCE_EPISODES} for config2, "
+                         "0 = off)")
+    ap.add_argument("--eps-windows", default="500,960",
+                    help="first episodes of the timed windows inside the schedule continuation")
+    ap.add_argument("--eps-window-steps", type=int, default=20)
+    ap.add_argument("--secondary", default="auto", choices=["auto", "none", "config3"],
+                    help="a second workload measured by the same ranks after the first (auto: configs[2], the "
+                         "shared-table workload with the int64 delta all-reduce, after the default config2)")
+    ap.add_argument("--secondary-scenarios", type=int, default=None)
+    ap.add_argument("--secondary-agents", type=int, default=None)
+    ap.add_argument("--secondary-horizon", type=int, default=None)
+    ap.add_argument("--secondary-steps", type=int, default=10)
+    ap.add_argument("--secondary-warmup", type=int, default=2)
+    ap.add_argument("--secondary-cpu-seconds", type=float, default=5.0)
     args = ap.parse_args()
     if args.gpus is not None and args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
@@ -674,192 +940,43 @@ def main():
 
     rank, world, local = dist_setup(args.gpus)
     args.gpus = world
-    from p2pmicrogrid_amd.dataset import apply_asset_mix, asset_mix, scenario_batch
-    DeviceCommunityBatch = engine_class()
-
-    S, N, R, T, q_dtype, shared, battery = WORKLOADS[args.workload]
-    hetero = args.workload in HETERO
-    S = args.scenarios or S
-    N = args.agents or N
-    R = R if args.rounds is None else args.rounds
-    T = args.horizon or T
-    q_dtype = args.q_dtype or q_dtype
     if args.workload == "config5":
-        return main_dqn(args, rank, world, local, S, N, R, T)
-    first = rank * S
-    inp = scenario_batch(S, N, T, first_scenario=first)
-    mix = None
-    if hetero:
-        mix = asset_mix(S, N, first_scenario=first, battery_j=BATTERY_J)
-        inp = apply_asset_mix(inp, mix)
-    eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=local, scenario_offset=first, shared_q=shared)
-    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
-    eng.set_profiles(inp.load_w, inp.pv_w)
-    eng.set_max_in(inp.max_in)
-    eng.set_temperatures(inp.t_in0, inp.t_m0)
-    del inp
-    if mix is not None:
-        eng.set_hp_levels(mix.hp_levels)
-        eng.set_battery(mix.battery_capacity)
-    elif battery:
-        eng.set_battery(BATTERY_J)
-    # episode metrics (+ the shared table's per-episode delta all-reduce, which needs RCCL)
-    xk = exchange_kind(args, world)
-    if xk == "host":  # rehearsal: int64 deltas and metrics summed over gloo
-        comm_err = "host-rehearsal exchange (no RCCL communicator)"
-    else:
-        comm_err = rccl_comm(eng, rank, world, required=shared)
-    record = ("reward", "cost")
-
-    def episode(e):
-        if shared:
-            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record,
-                            next_epsilon=epsilon_at(e + 1))
-            if world > 1 and xk == "host":
-                from p2pmicrogrid_amd.distributed import all_reduce_int64
-                eng.set_q_delta(all_reduce_int64(eng.get_q_delta(), world))
-            elif world > 1:
-                eng.allreduce_q_delta()
-            eng.apply_q_delta()
-            eng.reset_temperatures_philox(e + 1, 0.3)  # agent.reset() at the end of train_episode
-        else:  # the same reset, fused into the episode launch
-            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record, reset_sigma=0.3,
-                            next_epsilon=epsilon_at(e + 1))
-
-    for e in range(args.warmup):
-        episode(e)
-    eng.sync()
-    eng.reset_kernel_times()
-    # HIP events on every launch cost ~4 us per configs[1] episode: sample every 5th launch
-    timing_period = 5 if args.steps >= 20 else 1
-    eng.set_timing_period(timing_period)
-    barrier(world)
-    eng.sync()
-    t0 = time.perf_counter()
-    metrics = None
-    for k, e in enumerate(range(args.warmup, args.warmup + args.steps)):
-        episode(e)
-        if (k + 1) % args.metric_every == 0 or k + 1 == args.steps:
-            metrics = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
-    eng.sync()
-    barrier(world)
-    rank_times = all_gather_float(time.perf_counter() - t0, world)
-    dt = max(rank_times)
-    kms = eng.kernel_times()
-    coll = collective_record(eng, world, args.steps)
-    ep_reward = metrics[0] / metrics[1]
-    nranks = eng.comm_nranks() if not comm_err else 0
-    if shared and xk == "host":  # every replica's fingerprint, gathered over gloo
-        from p2pmicrogrid_amd.distributed import all_gather_concat
-        hashes = all_gather_concat(eng.table_hash_allgather().astype(np.uint64), world)
-    else:
-        hashes = eng.table_hash_allgather() if shared else None  # every replica of the shared table
-
-    steps_per_episode = S * N * T
-    value = world * steps_per_episode * args.steps / dt
-    q_bytes = 8 if q_dtype == "f64" else 4
-    if shared:
-        bpa = algorithmic_bytes_per_agent_step_shared(S * N, q_bytes, battery, outputs=len(record))
-        workload = (f"configs[2]: {S} scenarios/GPU x {N} agents (R={R}, T={T}) with battery storage, one shared "
-                    f"{q_dtype} Q-table, int64 delta all-reduce per episode, Philox exploration, train episodes")
-    elif hetero:
-        bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
-        workload = (f"configs[3]: {S} scenarios/GPU x {N} heterogeneous households (R={R}, T={T} = "
-                    f"{T // 96} days; no-PV / heat-pump size / battery mixes), per-agent {q_dtype} Q-tables, "
-                    f"Philox exploration, train episodes")
-    else:
-        bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
-        workload = (f"configs[1]: {S} scenarios/GPU x thesis community (N={N}, R={R}, T={T}), per-agent "
-                    f"{q_dtype} Q-tables, Philox exploration, train episodes")
-    kernel_ms = float(np.mean(kms)) if len(kms) else float("nan")
-    achieved = bpa * steps_per_episode / (kernel_ms * 1e-3) / 1e9
-    tj = args.traffic_json or os.path.join(
-        ROOT, "profiles", "pmc_traffic.json" if args.workload == "config2" else f"pmc_traffic_{args.workload}.json")
-    traffic = load_traffic(tj, workload)
+        S, N, R, T, _, _, _ = WORKLOADS["config5"]
+        R = R if args.rounds is None else args.rounds
+        main_dqn(args, rank, world, local, args.scenarios or S, args.agents or N, R, args.horizon or T)
+        return 0
+    sched = args.schedule_episodes
+    if sched is None:
+        sched = REFERENCE_EPISODES if args.workload == "config2" else 0
+    windows = [int(x) for x in args.eps_windows.split(",") if x.strip()]
+    out = run_tabular(args, rank, world, local, args.workload, S=args.scenarios, N=args.agents, R=args.rounds,
+                      T=args.horizon, q_dtype=args.q_dtype, steps=args.steps, warmup=args.warmup,
+                      cpu_seconds=args.cpu_seconds, schedule_to=sched, eps_windows=windows,
+                      window_steps=args.eps_window_steps)
+    sec_wl = args.secondary
+    if sec_wl == "auto":
+        sec_wl = "config3" if args.workload == "config2" else "none"
+    if sec_wl != "none" and sec_wl != args.workload:
+        # SURVEY §8d judges the roofline on configs[2]; at world > 1 its per-episode int64 delta
+        # all-reduce is the path's real exchange over xGMI, so the driver's scaling runs carry it too
+        try:
+            sec = run_tabular(args, rank, world, local, sec_wl, S=args.secondary_scenarios, N=args.secondary_agents,
+                              T=args.secondary_horizon, steps=args.secondary_steps, warmup=args.secondary_warmup,
+                              cpu_seconds=args.secondary_cpu_seconds)
+        except Exception as e:  # noqa: BLE001  (the primary line stands; the failure is reported in it)
+            print(f"bench.py: secondary workload {sec_wl} failed on rank {rank}: {type(e).__name__}: {e}",
+                  file=sys.stderr, flush=True)
+            sec = {"error": f"{type(e).__name__}: {e}", "workload": sec_wl}
+        if rank == 0:
+            for k in ("metric", "higher_is_better", "scaling", "vs_baseline", "n_gpus"):
+                sec.pop(k, None)
+            out["secondary"] = sec
     if rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "agent-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32 simulation, f64 Q-table" if q_dtype == "f64" else "f32",
-            "data": "synthetic profiles with the reference dataset schema (seed 42)",
-            "config": {"workload": workload, "scenarios_per_gpu": S, "agents_per_scenario": N,
-                       "rounds": R, "negotiation_rounds": R + 1, "horizon": T, "q_dtype": q_dtype, "shared_q": shared, "battery": battery,
-                       "agent_steps_per_step": world * steps_per_episode,
-                       "parallelism": (f"scenario-sharded x{world}, shared-table delta all-reduce (RCCL)" if shared
-                                       else f"scenario-sharded x{world} (replicas, no data-path collective)")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
-                         "kernel": eng.last_kernel(),
-                         "kernel_ms": kernel_ms,
-                         "algorithmic_bytes_per_agent_step": bpa,
-                         "algorithmic_bytes_per_launch": bpa * steps_per_episode,
-                         "timed_launches": int(len(kms)), "timing_period": timing_period},
-            "mean_episode_reward": ep_reward,
-            "rccl_nranks": nranks,
-            "rank_times_s": rank_times,
-        }
-        if os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
-            out["test_engine"] = os.environ["P2PMG_BENCH_TEST_ENGINE"]
-        if comm_err:
-            out["rccl_error"] = comm_err
-        if world > 1:
-            out["exchange"] = "host-rehearsal" if xk == "host" else "rccl"
-        if coll and xk != "host":
-            out["collective"] = coll
-        if shared:
-            out["table_replicas_identical"] = bool(np.all(hashes == hashes[0]))
-            assert out["table_replicas_identical"], f"shared-table replicas differ across ranks: {hashes}"
-        if traffic:
-            out["roofline"]["traffic_source"] = traffic.get("source")
-        if not shared and q_dtype == "f64" and N <= 8:  # the fast kernel's sector-granular traffic model
-            eps_mid = epsilon_at(args.warmup + args.steps // 2)
-            sm = sector_model_per_agent_step(N, R, eps_mid, battery or hetero)
-            sm["bytes_per_launch"] = sm["total"] * steps_per_episode
-            out["roofline"]["sector_model"] = sm
-        issue = issue_roofline(args.workload, kernel_ms)
-        if issue:
-            out["roofline"]["issue"] = issue
-        # What binds the kernel: achieved/peak/frac above stay the HBM roofline
-        # (algorithmic bytes); "bound" names the limit the measurements point to and
-        # "binding_frac" is the fraction against that limit.
-        if not (shared or battery or hetero) and q_dtype == "f64" and N == 2 and R == 1:
-            gather = gather_roofline(S * N, T, kernel_ms)
-            if gather:
-                out["roofline"]["gather_floor"] = gather
-                out["roofline"]["bound"] = "latency"  # one wave per CU: the dependent row-gather chain
-                out["roofline"]["binding_frac"] = gather["frac"]
-        elif hetero and q_dtype == "f64" and N == 4 and R == 1:
-            gather = gather_roofline(S * N, T, kernel_ms, stages=2, agents_per_wave=64, pool=400, rows=3,
-                                     source="r04_ubench_gather.jsonl")
-            if gather:  # two dependent gather round trips per step + the f64 battery rules on the chain
-                out["roofline"]["gather_floor"] = gather
-                out["roofline"]["bound"] = "latency"
-                out["roofline"]["binding_frac"] = gather["frac"]
-        elif shared and issue and issue["frac"] > 0.5:
-            out["roofline"]["bound"] = "valu-issue"  # every SIMD busy: VALU instructions per agent-step
-            out["roofline"]["binding_frac"] = issue["frac"]
-        if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline_all_cores("cpu_baseline", dict(
-                seconds=args.cpu_seconds, S=(64 if hetero else 256) if N <= 4 else 64, N=N, R=R, T=T, q_dtype=q_dtype,
-                shared=shared, battery=battery, hetero=hetero, t_sample=960 if T > 960 else 0), cpu_workers())
-            cb["os_cpu_count"] = os.cpu_count()
-            if not (shared or battery or hetero):  # the per-object loop restates the tabular path only
-                cb["per_object"] = cpu_baseline_per_object(min(args.cpu_seconds, 5.0), N=N, R=R, T=T)
-            out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

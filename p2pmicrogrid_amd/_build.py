@@ -57,7 +57,7 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=(),
     sources newer): the later ones wait, see a fresh library and return without compiling."""
     if out == LIB and not defines and not force and not needs_build():
         return LIB
-    tag = "main" if not defines else "_".join(d.replace("=", "") for d in defines)
+    tag = ARCH + ("_main" if not defines else "_" + "_".join(d.replace("=", "") for d in defines))
     obj_dir = os.path.join(ROOT, "build", "obj", tag)
     os.makedirs(obj_dir, exist_ok=True)
     with open(os.path.join(ROOT, "build", "obj", f"{tag}.lock"), "w") as lock:
@@ -65,12 +65,21 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=(),
         try:
             if out == LIB and not defines and not force and not needs_build():
                 return LIB  # another process built it while this one waited
-            return _build_locked(obj_dir, out, defines, jobs, verbose)
+            return _build_locked(obj_dir, out, defines, jobs, verbose, force)
         finally:
             fcntl.flock(lock, fcntl.LOCK_UN)
 
 
-def _build_locked(obj_dir: str, out: str, defines, jobs: int, verbose: bool) -> str:
+def hipcc_identity() -> str:
+    """The compiler's path and version line, part of every object's stamp."""
+    try:
+        v = subprocess.run([hipcc(), "--version"], capture_output=True, text=True, timeout=60).stdout
+    except (OSError, subprocess.SubprocessError):
+        v = ""
+    return hipcc() + " | " + " ".join(v.split())
+
+
+def _build_locked(obj_dir: str, out: str, defines, jobs: int, verbose: bool, force: bool = False) -> str:
     common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
               "-Wall", "-Wno-unused-function", "-Wno-pass-failed", f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
               *[d if d.startswith("-") else f"-D{d}" for d in defines]]  # "-..." entries: raw flags
@@ -81,24 +90,39 @@ def _build_locked(obj_dir: str, out: str, defines, jobs: int, verbose: bool) -> 
     pending = list(units)
     running = []
     objs = []
-    # an object newer than its source, every header and this script is reused (same tag = same flags)
+    # an object is reused only when it is newer than its source, every header and this script AND
+    # its stamp (the full compile command + the compiler's identity) matches; --force rebuilds all
     hdrs = [h if os.path.isabs(h) else os.path.join(CSRC, h) for h in HEADERS] + [os.path.abspath(__file__)]
     newest_hdr = max(os.path.getmtime(h) for h in hdrs if os.path.exists(h))
+    ident = hipcc_identity()
 
-    def fresh(src, obj):
-        return os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), newest_hdr)
+    def stamp_of(cmd):
+        return ident + "\n" + " ".join(cmd) + "\n"
 
+    def fresh(src, obj, cmd):
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) <= max(os.path.getmtime(src), newest_hdr):
+            return False
+        try:
+            return open(obj + ".cmd").read() == stamp_of(cmd)
+        except OSError:
+            return False
+
+    stamps = []
     while pending or running:
         while pending and len(running) < jobs:
             src, extra, o = pending.pop(0)
-            if fresh(src, os.path.join(obj_dir, o)):
-                objs.append(os.path.join(obj_dir, o))
+            obj = os.path.join(obj_dir, o)
+            cmd = [*common, *extra, "-c", src, "-o", obj]
+            if fresh(src, obj, cmd):
+                objs.append(obj)
                 continue
-            cmd = [*common, *extra, "-c", src, "-o", os.path.join(obj_dir, o)]
+            if os.path.exists(obj + ".cmd"):
+                os.remove(obj + ".cmd")
             if verbose:
                 print(" ".join(cmd), flush=True)
             running.append((subprocess.Popen(cmd), cmd))
-            objs.append(os.path.join(obj_dir, o))
+            stamps.append((obj, cmd))
+            objs.append(obj)
         if not running:
             break
         proc, cmd = running.pop(0)
@@ -106,6 +130,9 @@ def _build_locked(obj_dir: str, out: str, defines, jobs: int, verbose: bool) -> 
             for q, _ in running:
                 q.wait()
             raise subprocess.CalledProcessError(proc.returncode, cmd)
+    for obj, cmd in stamps:  # every compile succeeded: record what built each object
+        with open(obj + ".cmd", "w") as f:
+            f.write(stamp_of(cmd))
     tmp = f"{out}.{os.getpid()}.tmp"
     link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
     if verbose:

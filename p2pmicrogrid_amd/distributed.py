@@ -29,6 +29,9 @@ from typing import Callable, List, Optional
 import numpy as np
 
 
+DQN_TRAIN_SLOTS = 512  # dqn_train_kernel workgroups resident at once on MI355X: 256 CUs x 2
+
+
 @dataclass
 class Shard:
     rank: int
@@ -127,9 +130,10 @@ class ShardedTrainer:
     process group is nccl/RCCL, host otherwise).
     battery: kwargs for ``set_battery`` (scalars), enabling the storage rule.
     learner="dqn": grad_segments = the TOTAL gradient segment count (default: one per rank; must be
-    a multiple of world and divide n_scenarios) and agents_per_block fix the gradient's summation
-    structure, so a run is bit-identical for every world size that divides grad_segments; the
-    gradient exchange ("rccl" | "host") runs once per env step."""
+    a multiple of world and divide n_scenarios) and agents_per_block (default 0: ceil(agents of all
+    ranks / (512 x grad_segments)), a function of global sizes only) fix the gradient's summation
+    structure, so a run with the same grad_segments is bit-identical for every world size that
+    divides it; the gradient exchange ("rccl" | "host") runs once per env step."""
 
     def __init__(self, n_scenarios: int, n_agents: int = 2, rounds: int = 1, horizon: int = 96,
                  q_dtype: str = "f64", seed: int = 42, rank: int = 0, world: int = 1, device: int = 0,
@@ -147,7 +151,14 @@ class ShardedTrainer:
                 raise ValueError(f"grad_segments={G} must be a multiple of world={world} and divide "
                                  f"n_scenarios={n_scenarios}")
             self.grad_segments = G
-            dqn_kw = dict(learner="dqn", grad_segments=G // world, agents_per_block=agents_per_block)
+            if agents_per_block <= 0:
+                # rank-independent default: the block size must not follow the shard size (the device's
+                # own default, ceil(A_local / train slots), would change the summation order, and so the
+                # bits, with the world size).  ceil(A_total / (512 G)) gives every rank >= 512 train
+                # workgroups (2 per CU on 256 CUs) whatever the world, and depends on global sizes only.
+                agents_per_block = max(1, -(-(n_scenarios * n_agents) // (DQN_TRAIN_SLOTS * G)))
+            self.agents_per_block = int(agents_per_block)
+            dqn_kw = dict(learner="dqn", grad_segments=G // world, agents_per_block=self.agents_per_block)
             shared_q = True
             self.filled = False
         self.sh = shard(n_scenarios, rank, world)
