@@ -831,12 +831,16 @@ __device__ __forceinline__ Recip recip(float b) {
   const float y0 = __builtin_amdgcn_rcpf(b);
   return Recip{b, __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0), in_div_range(b)};
 }
+// ONE Newton correction of q0 = a y suffices (round 5): with y refined from v_rcp_f32 as in recip(),
+// q = fma(fma(-b, q0, a), y, q0) equals the IEEE quotient for every pair of 24-bit significands
+// (all 2^46 pairs checked on the GPU, scripts/div_exhaustive.hip, profiles/r05_div_exhaustive.jsonl),
+// v_rcp_f32 scales exactly with the divisor's exponent (same run, e in [-40, 40]), and inside the
+// range every step scales exactly with the operands' exponents (the residual stays representable),
+// so the significand pairs decide every case.  The second correction of rounds 1-4 was a no-op.
 __device__ __forceinline__ float fdiv_core(float a, const Recip& d) {
   const float q0 = a * d.y;
-  float r = __builtin_fmaf(-d.b, q0, a);
-  float q = __builtin_fmaf(r, d.y, q0);
-  r = __builtin_fmaf(-d.b, q, a);
-  q = __builtin_fmaf(r, d.y, q);
+  const float r = __builtin_fmaf(-d.b, q0, a);
+  const float q = __builtin_fmaf(r, d.y, q0);
   // a = +-0: the steps above give +0; the IEEE quotient carries sign(a) * sign(b) = sign(q0).
   // For every other a the sign of q already equals sign(q0), so the copy is exact either way.
   return __builtin_copysignf(q, q0);
@@ -1057,8 +1061,11 @@ __device__ __forceinline__ double battery_rule_pre(double balance, double& soc, 
   const double energy = energy_of(balance);
   const bool dis = balance > 0.0 && pr.avail_energy > 0.0;
   const bool chg = !dis && balance < 0.0 && !pr.full;
-  const double x = dis ? (energy <= pr.avail_energy ? energy : pr.avail_energy)    // min(energy, available_energy)
-                       : (-energy <= pr.avail_space ? -energy : pr.avail_space);  // min(-energy, available_space)
+  // min(energy, available_energy) / min(-energy, available_space) as v_min_f64 (IEEE minNum): in the
+  // launcher-verified domain every operand is finite, and where x is used both are positive (dis:
+  // energy > 0, avail_energy > 0; chg: -energy > 0, avail_space >= +0), so minNum returns what the
+  // reference's `a <= b ? a : b` does (equal values are the same double); 4 VALU instead of 9
+  const double x = dis ? fmin(energy, pr.avail_energy) : fmin(-energy, pr.avail_space);
   const double q1 = qpos64(x, rcap);     // x / capacity
   const double q2 = qpos64(x, b.r900);   // x / 900
   const double q3 = qpos64(q1, b.rse);   // (x / capacity) / sqrt(eff)
@@ -1740,7 +1747,7 @@ __device__ __forceinline__ bool in_range19(float x) {
   const float m = fabsf(x);
   return m == 0.0f || (m >= 0x1p-19f && m <= 0x1p19f);
 }
-// fdiv_core on a packed pair with the residual negated, r' = b q - a: the same quotient bit for
+// fdiv_core on a packed pair with the residual negated, r' = b q0 - a: the same quotient bit for
 // bit (round-to-nearest is sign-symmetric, and an exact-zero residual is +0 either way, which
 // leaves q unchanged), and for a = +-0 with a POSITIVE divisor (the only use: tot = |sum| > 0) it
 // keeps sign(a) without fdiv_core's copysign: q0 = +-0, r' = +0, q = fma(-0, y, +-0) = +-0.  (With
@@ -1748,10 +1755,8 @@ __device__ __forceinline__ bool in_range19(float x) {
 // fuzz test checks the positive-divisor domain.)  Both lanes round like the scalar fma.
 __device__ __forceinline__ pkf2 fdiv_core_pk(pkf2 a, pkf2 b, pkf2 y) {
   const pkf2 q0 = a * y;
-  pkf2 r = __builtin_elementwise_fma(b, q0, -a);
-  const pkf2 q1 = __builtin_elementwise_fma(-r, y, q0);
-  r = __builtin_elementwise_fma(b, q1, -a);
-  return __builtin_elementwise_fma(-r, y, q1);
+  const pkf2 r = __builtin_elementwise_fma(b, q0, -a);
+  return __builtin_elementwise_fma(-r, y, q0);  // one correction, as fdiv_core
 }
 // episode_sq16_kernel: episode_kernel's shared-table path for 16-agent scenarios (configs[2]),
 // rebuilt for throughput: 1M scenarios keep every SIMD busy, so the cost is instructions per
