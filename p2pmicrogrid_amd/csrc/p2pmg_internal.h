@@ -23,6 +23,7 @@ struct EpisodeParams {
   int n_env;                 // 1 (shared environment) or S (one per scenario)
   const float* env;          // [T][n_env][kEnvStride] time-major
   const float2* prof;        // [T][A] {load_w, pv_w}
+  const uint2* sqp;          // sq16 path: [T][A] {bits(balance), it * 8000 + ib * 20} (sq16_prep_kernel)
   const float* max_in;       // [A]
   float* t_in;               // [A] in/out
   float* t_m;                // [A] in/out
@@ -165,6 +166,8 @@ hipError_t launch_general_part8(const EpisodeParams& p, int q_dtype, hipStream_t
 hipError_t launch_rule_episode(const EpisodeParams& p, float* hp_on, hipStream_t stream);
 // shared table, N = 16, R <= 1 (configs[2]): episode_sq16_kernel; records packed like the fast path
 hipError_t launch_episode_sq16(const EpisodeParams& p, int q_dtype, hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
+// its per-upload pre-pass: out = p.sqp's contents from p.env, p.prof, p.max_in
+hipError_t launch_sq16_prep(const EpisodeParams& p, uint2* out, hipStream_t stream);
 constexpr size_t kFastRecBytes = 32;  // one packed record row per agent-step (FastRec)
 constexpr int kFastBatMaxR1 = 2;      // episode_fast_kernel's battery variants: R + 1 <= 2
 // which: 0..4 reward, cost, grid, p2p, tin ([T][A] f32); 5 action (u8), 6 index (i32) [T][R+1][A]

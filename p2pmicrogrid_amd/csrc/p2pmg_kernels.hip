@@ -1845,7 +1845,8 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   // values live across the loop than three running offsets and their wrap points)
   const float* envb = p.env + (size_t)s_env * kEnvStride;
   const uint32_t env_step = (uint32_t)p.n_env * kEnvStride;
-  const float2* profb = p.prof + a;
+  // the policy-independent per-step words {balance, it * 8000 + ib * 20} (sq16_prep_kernel)
+  const uint2* sqpb = p.sqp + a;
   const uint32_t A32 = (uint32_t)p.A;
   const uint32_t* codes_a = p.codes + a;
   const uint32_t code_step = (uint32_t)W * A32;
@@ -1865,25 +1866,21 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
 
   EnvRow e0 = load_env(envb);
   EnvRow e1 = load_env(envb + e1o);
-  const float2 f0 = profb[0];
-  float2 f1 = profb[f1o];
-  auto step_idx = [&](float time_t, float time_n, float bal, float2 fn, float t_in) {
+  const uint2 w0 = sqpb[0];
+  uint2 w1 = sqpb[f1o];
+  // step t's state: the balance and the time / balance part of the row offset come precomputed
+  // (w: step t, wn: step t + 1 for the next-state row); only the temperature bin depends on the
+  // policy: rl.py:89-95 as one v_med3 + convert (clamp_bin_f == clamp_bin for every non-NaN value)
+  auto step_idx = [&](uint2 w, uint2 wn, float t_in) {
     StepIdx st;
-    st.bal = bal;
-    st.baln = fdiv_b(fn.x - fn.y, rmi);
+    st.bal = __uint_as_float(w.x);
     const float dt = t_in - k.setpoint;
     const float tnorm = margin_one() ? dt : fdiv_b(dt, rmargin);
-    // rl.py:89-95 bins of the 20-state axes (the launcher sends this kernel 20^4 tables only), each
-    // as one v_med3 + convert (clamp_bin_f == clamp_bin for every non-NaN value), row offsets in
-    // 24-bit multiplies
-    st.it = clamp_bin_f(time_t * 20.0f, 19.0f);
     st.iT = clamp_bin_f(((tnorm + 1.0f) / 2.0f) * 18.0f + 1.0f, 19.0f);
-    st.ib = clamp_bin_f(((bal + 1.0f) / 2.0f) * 20.0f, 19.0f);
-    st.strip = __umul24(__umul24(__umul24((uint32_t)st.it, 20u) + (uint32_t)st.iT, 20u) + (uint32_t)st.ib, 20u);
-    const int itn = clamp_bin_f(time_n * 20.0f, 19.0f);
-    const int ibn = clamp_bin_f(((st.baln + 1.0f) / 2.0f) * 20.0f, 19.0f);
-    st.nrow = __umul24(__umul24(__umul24((uint32_t)itn, 20u) + (uint32_t)st.iT, 20u) + (uint32_t)ibn, 20u) +
-              (uint32_t)ip_zero;
+    const uint32_t tT = __umul24((uint32_t)st.iT, 400u);
+    st.strip = w.y + tT;
+    st.nrow = wn.y + tT + (uint32_t)ip_zero;
+    st.it = (int)w.y;  // it * 8000 + ib * 20: the records' bins are w.y / 20 (records only)
     return st;
   };
   // the shared table's rows as 32-bit offsets from its (uniform) base: global_load's SGPR-base +
@@ -1893,7 +1890,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   auto gatq = [&](uint32_t row) __attribute__((always_inline)) {
     return gather_row(reinterpret_cast<const QT*>(qb + (row << kRowShift)));
   };
-  StepIdx st = step_idx(e0.time, e1.time, fdiv_b(f0.x - f0.y, rmi), f1, tin);
+  StepIdx st = step_idx(w0, w1, tin);
   // R + 1 = 2 in-kernel Philox: one block holds the codes of two steps (p2pmg_device.h), computed
   // at the even step and kept for the odd one in the code word's unused high half
   constexpr bool kPair = R1 == 2 && TRAIN;
@@ -1917,7 +1914,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   for (int t = 0; t < T; ++t) {
     const uint32_t t1n = t + 1 == T ? 0u : (uint32_t)t + 1u;  // step t + 1 (mod T)
     const EnvRow e2 = load_env(envb + t2 * env_step);
-    const float2 f2 = profb[t2 * A32];
+    const uint2 w2 = sqpb[t2 * A32];
     const CodeWords cw1r = step_codes(p, codes_a, t1n * code_step, (int)t1n, a, W, !kPair);
     const float balw = st.bal * mi;
     float row[N];
@@ -2018,7 +2015,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     // RC update and the next step's rows
     float tin1 = tin, tm1 = tm;
     rc_update(k, e0.t_out, hp, tin1, tm1);
-    const StepIdx st1 = step_idx(e1.time, e2.time, st.baln, f2, tin1);
+    const StepIdx st1 = step_idx(w1, w2, tin1);
     uint64_t cw1 = code_word_t<TRAIN>(p, cw1r);
     if constexpr (kPair) {
       if (rng1) cw1 = (t1n & 1u) ? ((cw >> 32) | 0xFFFFFFFF00000000ull) : block2(t1n >> 1);
@@ -2075,7 +2072,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     if constexpr (narrow) {
       *reinterpret_cast<float2*>(__builtin_assume_aligned(rec_ptr, 8)) = make_float2(rw, cost);
     } else {
-      const uint32_t bins = (uint32_t)(st.it * D.T() * D.b() + st.ib) | ((uint32_t)st.iT << 16);
+      const uint32_t bins = ((uint32_t)st.it / 20u) | ((uint32_t)st.iT << 16);  // it * 400 + ib
       float4* rp = reinterpret_cast<float4*>(__builtin_assume_aligned(rec_ptr, 16));
       rp[0] = make_float4(rw, cost, g, pp);
       rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
@@ -2101,7 +2098,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
     tm = tm1;
     e0 = e1;
     e1 = e2;
-    f1 = f2;
+    w1 = w2;
     t2 = t2 + 1u == T32 ? 0u : t2 + 1u;
     st = st1;
     cw = cw1;
@@ -2296,12 +2293,53 @@ __global__ void q_unpack_kernel(size_t rows, int na, const S* src, D* dst) {
   for (int c = 0; c < na; ++c) dst[k * na + c] = (D)src[k * kQPad + c];
 }
 
+// [A][T] load / pv (the host's per-agent rows) -> [T][A] float2 (time-major, one coalesced 8-B load
+// per lane per step): a 32 x 32 tile transposed through LDS, so the reads are 128-B runs of one
+// agent's steps and the writes 256-B runs of one step's agents (round 5; the per-element form read
+// with stride T, 32x the input in fetched sectors).  Block (32, 8), tile [agent][step] padded to 33.
 #if P2PMG_IN_PART(0)
-__global__ void prof_pack_kernel(int A, int T, const float* load_w, const float* pv_w, float2* prof) {
+__global__ __launch_bounds__(256) void prof_pack_kernel(int A, int T, const float* __restrict__ load_w,
+                                                        const float* __restrict__ pv_w, float2* __restrict__ prof) {
+  __shared__ float tl[32][33], tv[32][33];
+  const int tx = (int)threadIdx.x, ty = (int)threadIdx.y;
+  const int a0 = (int)blockIdx.x * 32, t0 = (int)blockIdx.y * 32;  // grid.x: agents (grid.y <= 65535)
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int a = a0 + ty + k, t = t0 + tx;
+    if (a < A && t < T) {
+      const size_t src = (size_t)a * T + t;
+      tl[ty + k][tx] = load_w[src];
+      tv[ty + k][tx] = pv_w[src];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int t = t0 + ty + k, a = a0 + tx;
+    if (a < A && t < T) prof[(size_t)t * A + a] = make_float2(tl[tx][ty + k], tv[tx][ty + k]);
+  }
+}
+#endif
+
+// sq16_prep_kernel: the policy-independent part of episode_sq16_kernel's per-step state, once per
+// input upload (the runtime reruns it when env, profiles or max_in change): per (t, a) the agent's
+// balance (load - pv) / max_in (agent.py:172-176, the IEEE quotient the kernel's guarded fast
+// division returns) and the table offset of its time and balance bins, it * 8000 + ib * 20
+// (rl.py:89-95 on the 20^4 table the sq16 path serves; the temperature bin is added in the kernel).
+// The episode kernel then reads one 8-B word per agent-step instead of {load, pv} and skips the
+// division and three of the four bins of every step.
+#if P2PMG_IN_PART(5)
+__global__ void sq16_prep_kernel(const EpisodeParams p, uint2* __restrict__ out) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
-  if (k >= (size_t)A * T) return;
-  const int t = (int)(k / A), a = (int)(k % A);
-  prof[k] = make_float2(load_w[(size_t)a * T + t], pv_w[(size_t)a * T + t]);
+  if (k >= (size_t)p.A * p.T) return;
+  const int t = (int)(k / (size_t)p.A), a = (int)(k % (size_t)p.A);
+  const int s_env = p.n_env == 1 ? 0 : a / p.N;
+  const float time = p.env[((size_t)t * p.n_env + s_env) * kEnvStride];
+  const float2 f = p.prof[k];
+  const float bal = fdiv_ieee(f.x - f.y, p.max_in[a]);
+  const int it = clamp_bin_f(time * 20.0f, 19.0f);
+  const int ib = clamp_bin_f(((bal + 1.0f) / 2.0f) * 20.0f, 19.0f);
+  out[k] = make_uint2(__float_as_uint(bal), (uint32_t)(it * 8000 + ib * 20));
 }
 #endif
 
@@ -2664,9 +2702,19 @@ hipError_t launch_fdiv64_check(int n, const double* a, const double* b, double* 
 
 #if P2PMG_IN_PART(0)
 hipError_t launch_prof_pack(int A, int T, const float* load_w, const float* pv_w, float2* prof, hipStream_t stream) {
-  const size_t n = (size_t)A * T;
+  if ((size_t)A * T == 0) return hipSuccess;
+  if ((T + 31) / 32 > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(prof_pack_kernel, dim3((A + 31) / 32, (T + 31) / 32), dim3(32, 8), 0, stream, A, T, load_w, pv_w,
+                     prof);
+  return hipGetLastError();
+}
+#endif
+
+#if P2PMG_IN_PART(5)
+hipError_t launch_sq16_prep(const EpisodeParams& p, uint2* out, hipStream_t stream) {
+  const size_t n = (size_t)p.A * p.T;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(prof_pack_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, A, T, load_w, pv_w, prof);
+  hipLaunchKernelGGL(sq16_prep_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, p, out);
   return hipGetLastError();
 }
 #endif

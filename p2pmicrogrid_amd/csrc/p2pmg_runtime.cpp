@@ -46,6 +46,8 @@ struct p2pmg_ctx {
   float* env = nullptr;
   int n_env = 0;
   float2* prof = nullptr;
+  uint2* sqp = nullptr;             // sq16 path: per-upload step words (launch_sq16_prep), lazily allocated
+  long long sqp_version = -1;       // inputs_version they were computed for
   float* max_in = nullptr;
   float* t_in = nullptr;
   float* t_m = nullptr;
@@ -340,6 +342,7 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dfree(c->env);
   dfree(c->prof);
+  dfree(c->sqp);
   dfree(c->max_in);
   dfree(c->t_in);
   dfree(c->t_m);
@@ -762,6 +765,13 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     if (args->record && !c->rec_pack)
       HIP_TRY(c, hipMalloc(&c->rec_pack, (size_t)c->T * c->A * p2pmg::kFastRecBytes));
     p.rec_pack = c->rec_pack;
+    // the step words {balance, time / balance row offset}: recomputed after any input upload
+    if (!c->sqp) HIP_TRY(c, dmalloc(&c->sqp, (size_t)c->T * c->A));
+    if (c->sqp_version != c->inputs_version) {
+      HIP_TRY(c, p2pmg::launch_sq16_prep(p, c->sqp, c->stream));
+      c->sqp_version = c->inputs_version;
+    }
+    p.sqp = c->sqp;
   }
   // fast / sq16: only {reward, cost} requested -> 8-B record rows
   p.rec_narrow = (fast || sq16) && (args->record & ~(P2PMG_REC_REWARD | P2PMG_REC_COST)) == 0 ? 1 : 0;
