@@ -409,7 +409,12 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     from p2pmicrogrid_amd.dataset import scenario_batch
     first = rank * S
     inp = scenario_batch(S, N, T, first_scenario=first)
-    eng = dqn_engine_class()(S, N, R, T, shared=True, device=local, scenario_offset=first, init_seed=0)
+    dkw = {}
+    if args.grad_segments:  # the split path (segment fold -> exchange -> dqn_adam_shared_kernel) at any world
+        dkw["grad_segments"] = args.grad_segments
+    if args.agents_per_block:
+        dkw["agents_per_block"] = args.agents_per_block
+    eng = dqn_engine_class()(S, N, R, T, shared=True, device=local, scenario_offset=first, init_seed=0, **dkw)
     eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
     eng.set_profiles(inp.load_w, inp.pv_w)
     eng.set_max_in(inp.max_in)
@@ -921,6 +926,10 @@ def main():
     ap.add_argument("--eps-windows", default="500,960",
                     help="first episodes of the timed windows inside the schedule continuation")
     ap.add_argument("--eps-window-steps", type=int, default=20)
+    ap.add_argument("--grad-segments", type=int, default=0,
+                    help="config5: gradient segments of this rank (0 = one; > 1 takes the split fold -> exchange "
+                         "-> Adam path even at world 1)")
+    ap.add_argument("--agents-per-block", type=int, default=0, help="config5: agents per train workgroup (0 = auto)")
     ap.add_argument("--secondary", default="auto", choices=["auto", "none", "config3"],
                     help="a second workload measured by the same ranks after the first (auto: configs[2], the "
                          "shared-table workload with the int64 delta all-reduce, after the default config2)")

@@ -598,7 +598,7 @@ class OracleDQNBatch:
                     c = codes[t, r]
                     a = np.where(c == GREEDY, greedy, c.astype(np.int64))
                 else:
-                    u, ra = philox.decision_draws(seed, episode, gids.ravel(), t, r, R)
+                    u, ra = philox.decision_draws(seed, episode, gids.ravel(), t, r, R, eps=philox.launch_eps(eps_arr))
                     a = np.where(u.reshape(S, N) < eps_arr, ra.reshape(S, N), greedy)
                 hp = lv[a]
                 out = (bal * mi) + hp                                      # agent.py:210

@@ -17,8 +17,11 @@ word per negotiation round, so one block serves four rounds (two agent-steps at 
     w    = x[k % 4]
     u    = w / 2**32                                           (exact in f64)
     explore <=> u < epsilon   (f64 compare, as rl.py:101)
-    act  = w % 3   (used only when exploring: given u < epsilon, w is uniform on [0, thr),
-                    thr = ceil(epsilon * 2**32), so w % 3 is uniform up to 1 / thr)
+    act  = w % 3   when thr = ceil(epsilon * 2**32) >= 2**24 (used only when exploring: given
+                   u < epsilon, w is uniform on [0, thr), so w % 3 is uniform up to 1 / thr <= 2**-24);
+           v % 3   when thr < 2**24 (small epsilon: w itself is below thr, so w % 3 would be biased),
+                   v = word k % 4 of the block ctr = (k // 4, episode, agent_global, TAG_ACTION),
+                   independent of the explore test (rl.py:110-111 draws the action separately)
 T0 draws at an episode start (tag TAG_T0, ctr = (0, episode, agent, TAG_T0)):
     Box-Muller in f64 on u1 = (x0 + 0.5) / 2**32, u2 = (x1 + 0.5) / 2**32;
     T_in = f32(setpoint + 0.3 * z0), T_m = f32(setpoint + 0.3 * z1)   (heating.py:149-152)
@@ -35,6 +38,17 @@ MASK32 = np.uint64(0xFFFFFFFF)
 
 TAG_DECISION = 0x5EED0004  # one word per round, four rounds per block (0x5EED0003: two rounds per block)
 TAG_T0 = 0x5EED0002
+TAG_ACTION = 0x5EED0005    # small epsilon: the explore actions' own block
+SMALL_EPS_THR = 1 << 24
+
+
+def eps_threshold(eps: float):
+    """(thr, all): w / 2**32 < eps  <=>  all or w < thr (p2pmg_internal.h::eps_threshold)."""
+    c = np.ceil(float(eps) * 4294967296.0)
+    if not c > 0.0:
+        c = 0.0
+    all_ = c >= 4294967296.0
+    return (0xFFFFFFFF if all_ else int(c)), bool(all_)
 
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):
@@ -59,8 +73,18 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
     return c0, c1, c2, c3
 
 
-def decision_draws(seed: int, episode: int, agents, t: int, r: int, rounds: int):
-    """(u f64, action int) for each agent id in ``agents`` at (episode, t, r); ``rounds`` = R."""
+def launch_eps(eps_arr) -> float:
+    """The one epsilon of a Philox-mode launch (the device takes a single threshold per launch)."""
+    e = np.asarray(eps_arr, dtype=np.float64)
+    if not np.all(e == e.flat[0]):
+        raise ValueError("Philox mode draws with one epsilon per launch")
+    return float(e.flat[0])
+
+
+def decision_draws(seed: int, episode: int, agents, t: int, r: int, rounds: int, eps=None):
+    """(u f64, action int) for each agent id in ``agents`` at (episode, t, r); ``rounds`` = R.
+    eps (the launch's epsilon, one value): below 2**-8 (thr < 2**24) the action comes from the
+    TAG_ACTION block; None = the large-epsilon layout (action = w % 3)."""
     agents = np.asarray(agents, dtype=np.uint64)
     k0 = seed & 0xFFFFFFFF
     k1 = (seed >> 32) & 0xFFFFFFFF
@@ -68,7 +92,12 @@ def decision_draws(seed: int, episode: int, agents, t: int, r: int, rounds: int)
     x = philox4x32_10(k // 4, episode, agents, TAG_DECISION, k0, k1)
     w = x[k % 4]
     u = w.astype(np.float64) / 4294967296.0
-    act = (w % np.uint64(3)).astype(np.int64)
+    aw = w
+    if eps is not None:
+        thr, all_ = eps_threshold(eps)
+        if not all_ and thr < SMALL_EPS_THR:
+            aw = philox4x32_10(k // 4, episode, agents, TAG_ACTION, k0, k1)[k % 4]
+    act = (aw % np.uint64(3)).astype(np.int64)
     return u, act
 
 

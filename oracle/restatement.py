@@ -439,7 +439,7 @@ class OracleBatch:
                     c = codes[t, r]
                     a = np.where(c == GREEDY, greedy, c.astype(np.int64))
                 else:
-                    u, ra = philox.decision_draws(seed, episode, gids.ravel(), t, r, R)
+                    u, ra = philox.decision_draws(seed, episode, gids.ravel(), t, r, R, eps=philox.launch_eps(eps_arr))
                     u = u.reshape(S, N)
                     ra = ra.reshape(S, N)
                     a = np.where(u < eps_arr, ra, greedy)

@@ -57,14 +57,22 @@ __device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32
 }
 constexpr uint32_t kTagDecision = 0x5EED0004u;  // one 32-bit word per round (oracle/philox.py)
 constexpr uint32_t kTagT0 = 0x5EED0002u;
+constexpr uint32_t kTagAction = 0x5EED0005u;    // small epsilon: the explore actions' own block
+constexpr uint32_t kSmallEpsThr = 1u << 24;     // eps < 2^-8: below it the actions come from kTagAction
 
 // Philox exploration stream (oracle/philox.py::decision_draws; QActor.select_action rl.py:100-111):
 // round r of step t of agent gid uses word k % 4 of the block ctr = (k / 4, episode, gid,
 // kTagDecision), k = t (R + 1) + r.  The agent explores when w / 2^32 < eps (w < thr, eps_threshold)
-// and then takes action w % 3: given w < thr, w is uniform on [0, thr), so w % 3 is uniform up to
-// 1 / thr.  One word per round: a block serves four rounds (two steps at R = 1).  255 = greedy.
-__device__ __forceinline__ uint32_t decision_code(uint32_t w, uint32_t thr, int all) {
-  return (all || w < thr) ? w % 3u : 255u;
+// and then takes a uniformly drawn action (rl.py:110-111 draws it separately from the explore test):
+//   thr >= 2^24 (eps >= 2^-8, every tabular run: its floor is 0.1): action w % 3 -- given w < thr,
+//     w is uniform on [0, thr), so w % 3 is uniform up to 1 / thr <= 2^-24;
+//   thr < 2^24 (small eps, e.g. the DQN's unfloored 0.9^e decay): w % 3 of a w below a small thr
+//     would be biased (every w < 3: one fixed action), so the action is word k % 4 of the block
+//     (k / 4, episode, gid, kTagAction), independent of the explore test, % 3 (bias <= 2^-32).
+// The branch is kernel-uniform (thr is a launch argument).  One word per round: a block serves four
+// rounds (two steps at R = 1).  255 = greedy.
+__device__ __forceinline__ uint32_t decision_code(uint32_t w, uint32_t act_word, uint32_t thr, int all) {
+  return (all || w < thr) ? act_word % 3u : 255u;
 }
 // the four codes of block blk, byte j = word j
 __device__ __forceinline__ uint32_t philox_block_codes(uint32_t blk, uint32_t episode, uint32_t gid, uint32_t thr,
@@ -74,8 +82,13 @@ __device__ __forceinline__ uint32_t philox_block_codes(uint32_t blk, uint32_t ep
   // loop they would be 20 uniform values held across it
   asm volatile("" : "+s"(k0), "+s"(k1));
   philox4x32_10(c0, c1, c2, c3, k0, k1);
-  return decision_code(c0, thr, all) | (decision_code(c1, thr, all) << 8) | (decision_code(c2, thr, all) << 16) |
-         (decision_code(c3, thr, all) << 24);
+  uint32_t a0 = c0, a1 = c1, a2 = c2, a3 = c3;
+  if (!all && thr < kSmallEpsThr) {
+    a0 = blk, a1 = episode, a2 = gid, a3 = kTagAction;
+    philox4x32_10(a0, a1, a2, a3, k0, k1);
+  }
+  return decision_code(c0, a0, thr, all) | (decision_code(c1, a1, thr, all) << 8) |
+         (decision_code(c2, a2, thr, all) << 16) | (decision_code(c3, a3, thr, all) << 24);
 }
 // every round's code of step t, byte r (bytes r >= R1: 255); R1 <= 8
 __device__ __forceinline__ uint64_t philox_step_codes(int t, int R1, uint32_t episode, uint32_t gid, uint32_t thr,

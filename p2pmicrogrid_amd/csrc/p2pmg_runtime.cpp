@@ -40,6 +40,7 @@ struct p2pmg_ctx {
   std::vector<hipEvent_t> cring;  // 2 * kCRing events: start/stop of each data-path RCCL all-reduce
   long long n_coll = 0;           // collectives recorded since the last reset
   double coll_folded_ms = 0.0;    // durations of ring slots already reused (p2pmg_collective_ms)
+  long long n_coll_folded = 0;    // collectives whose durations are in coll_folded_ms
   int timing_period = 1;          // episode launches: stamp timing events on every k-th one
   long long n_launch = 0;         // episode launches since the last reset
   // device buffers
@@ -907,6 +908,7 @@ int p2pmg_reset_kernel_times(p2pmg_ctx* c) {
   c->n_launch = 0;
   c->n_coll = 0;
   c->coll_folded_ms = 0.0;
+  c->n_coll_folded = 0;
   return P2PMG_OK;
 }
 
@@ -1184,14 +1186,17 @@ static hipError_t coll_mark(p2pmg_ctx* c, int end) {
     }
   }
   const int slot = (int)(c->n_coll % p2pmg_ctx::kCRing);
-  if (!end && c->n_coll >= p2pmg_ctx::kCRing) {
+  if (!end && c->n_coll >= p2pmg_ctx::kCRing && c->n_coll_folded == c->n_coll - p2pmg_ctx::kCRing) {
     // the slot's previous pair (kCRing collectives ago) is about to be overwritten: fold its
-    // duration into the running total first, so p2pmg_collective_ms counts every collective
+    // duration into the running total first, so p2pmg_collective_ms counts every collective.
+    // Once per collective: a start whose collective then failed (no end mark, n_coll unchanged)
+    // is followed by another start on the same slot, which must not fold the slot again
     float ms = 0.0f;
     hipError_t e = hipEventSynchronize(c->cring[2 * slot + 1]);
     if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->cring[2 * slot], c->cring[2 * slot + 1]);
     if (e != hipSuccess) return e;
     c->coll_folded_ms += ms;
+    c->n_coll_folded++;
   }
   const hipError_t e = hipEventRecord(c->cring[2 * slot + end], c->stream);
   if (end) c->n_coll++;
@@ -1641,9 +1646,10 @@ static int dqn_gather_segments(p2pmg_ctx* c) {
 }
 
 static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
-  // one env step trains every network once (community.py:158-168)
-  for (auto& st : c->d_steps) ++st;
-  d.lr_t = adam_lr(c->dcfg, c->d_steps[0]);
+  // one env step trains every network once (community.py:158-168); the Adam step counters advance
+  // only once every launch of the step is enqueued (a failed exchange leaves weights and counters
+  // at the previous step: the Adam launch that would change the weights was not issued)
+  d.lr_t = adam_lr(c->dcfg, c->d_steps[0] + 1);
   d.lr_net = same ? nullptr : c->d_lr + (size_t)d.t * c->d_steps.size();
   if (!d.fused_sample) HIP_TRY(c, p2pmg::launch_dqn_sample(d, c->stream));
   if (c->n_nets == 1) {
@@ -1652,7 +1658,7 @@ static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
       HIP_TRY(c, p2pmg::launch_dqn_reduce_adam(d, 1, true, c->stream));
     } else {
       HIP_TRY(c, p2pmg::launch_dqn_reduce_adam(d, c->d_seg_local, false, c->stream));
-      if (c->nranks > 1) {
+      if (c->nranks > 1 || c->comm) {  // a communicator gathers even at world 1 (the RCCL path, tested)
         const int rc = dqn_gather_segments(c);
         if (rc != P2PMG_OK) return rc;
       }
@@ -1661,6 +1667,7 @@ static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
   } else {
     HIP_TRY(c, p2pmg::launch_dqn_train(d, c->A, false, c->stream));
   }
+  for (auto& st : c->d_steps) ++st;
   return P2PMG_OK;
 }
 

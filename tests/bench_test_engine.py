@@ -64,9 +64,11 @@ class BenchOracleEngine(OracleEngine):
 class BenchOracleDQNEngine:
     """The DeviceDQNBatch calls main_dqn makes, on oracle/dqn.py (one shared network)."""
 
-    def __init__(self, S, N, R, T, shared=True, device=0, scenario_offset=0, init_seed=0, seed=42):
+    def __init__(self, S, N, R, T, shared=True, device=0, scenario_offset=0, init_seed=0, seed=42, grad_segments=1,
+                 agents_per_block=0):
         from oracle_engine import OracleDQNEngine
-        self._e = OracleDQNEngine(Shard(0, 1, scenario_offset, S), S, N, R, T, "f32", device, seed)
+        self._e = OracleDQNEngine(Shard(0, 1, scenario_offset, S), S, N, R, T, "f32", device, seed,
+                                  grad_segments=grad_segments, agents_per_block=agents_per_block)
         self.S, self.N, self.R, self.T = S, N, R, T
 
     def __getattr__(self, name):  # set_env, set_profiles, ..., run_episode, episode_reward, get_weights

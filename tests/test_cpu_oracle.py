@@ -198,3 +198,19 @@ def test_rule_community_api_only_runs():
     assert com._rounds == 0 and {type(a).__name__ for a in com.agents} == {"RuleAgent"}
     with pytest.raises(AttributeError):
         com.train_episode()
+
+
+def test_small_epsilon_action_words_are_independent_and_uniform():
+    """Below epsilon 2^-8 the explore actions come from the TAG_ACTION block: uniform
+    and unrelated to the explore word; at larger epsilon the action is w % 3 of the explore word."""
+    agents = np.arange(300000)
+    u, a_big = philox.decision_draws(42, 3, agents, 5, 1, 1, eps=0.5)
+    w = np.round(u * 4294967296.0).astype(np.uint64)
+    assert np.array_equal(a_big, (w % np.uint64(3)).astype(np.int64))
+    u2, a_small = philox.decision_draws(42, 3, agents, 5, 1, 1, eps=1e-9)
+    assert np.array_equal(u, u2)  # the explore test itself does not change
+    shares = np.bincount(a_small, minlength=3) / len(agents)
+    assert np.all(np.abs(shares - 1 / 3) < 0.005), shares
+    assert np.mean(a_small == a_big) < 0.36  # independent of the explore word (1/3 by chance)
+    thr, all_ = philox.eps_threshold(2.0 ** -8)
+    assert thr == 1 << 24 and not all_

@@ -87,6 +87,21 @@ def test_shared_battery_hetero_match_oracle(N, R, T, q_dtype, shared, battery, h
     _cmp(ob.run_episode("greedy"), eng.get_records(REC), "greedy")
 
 
+def test_sq16_small_epsilon_matches_oracle():
+    """configs[2]'s kernel (shared table, N = 16, battery) at epsilon < 2^-8: the exploring lanes'
+    actions come from the TAG_ACTION block (p2pmg_device.h::philox_block_codes), as in the oracle."""
+    S, N, R, T = 64, 16, 1, 48
+    eng, ob = _setup(S, N, R, T, "f32", True, True, False, seed=23)
+    for e in range(2):
+        eng.run_episode("train", "philox", episode=e, epsilon=0.0035, record=REC)
+        assert eng.last_kernel().startswith("episode_sq16_kernel<")
+        out = ob.run_episode("train", rng="philox", episode=e, eps=0.0035)
+        _cmp(out, eng.get_records(REC), ("small-eps", e))
+        assert np.array_equal(eng.get_q_delta().reshape(-1, 3), ob.q_delta)
+        eng.apply_q_delta()
+        ob.apply_q_delta()
+
+
 @pytest.mark.parametrize("N", [2, 4])
 def test_battery_fast_kernel_narrow_records_match_oracle(N):
     """configs[3] shape on the battery fast kernel: only {reward, cost} requested -> 8-B record rows

@@ -151,6 +151,30 @@ def test_dqn_shared_network_two_ranks_match_single_context():
         assert np.allclose(means1, means2, rtol=0, atol=1e-9)
 
 
+def test_dqn_rccl_gather_world1_matches_single_context():
+    """The RCCL half of the shared DQN network's gradient exchange on one GPU: a world-1
+    communicator with 2 gradient segments takes the split path (segment fold -> in-place
+    ncclAllGather -> dqn_adam_shared_kernel); weights, target and Adam state equal the context without
+    a communicator bit for bit, and every gather is counted by the collective timer."""
+    from p2pmicrogrid_amd.engine import comm_unique_id
+    single = ShardedTrainer(DQN_S, N, R, T, device=0, **DQN_KW)
+    means1 = _dqn_episodes(single)
+    w1, t1, v1 = (single.eng.get_weights(k) for k in ("online", "target", "adam_v"))
+    single.eng.close()
+    tr = ShardedTrainer(DQN_S, N, R, T, device=0, **DQN_KW)
+    tr.eng.comm_init(comm_unique_id(), 0, 1)
+    assert tr.eng.comm_nranks() == 1
+    tr.fill_buffers()
+    tr.eng.reset_kernel_times()
+    means2 = _dqn_episodes(tr)
+    total, calls = tr.eng.collective_ms()
+    assert calls == EPISODES * T and total > 0.0  # one all-gather per training env step
+    w2, t2, v2 = (tr.eng.get_weights(k) for k in ("online", "target", "adam_v"))
+    tr.eng.close()
+    assert np.array_equal(w1, w2) and np.array_equal(t1, t2) and np.array_equal(v1, v2)
+    assert np.allclose(means1, means2, rtol=0, atol=0)
+
+
 def test_rccl_metrics_and_table_hash_world1():
     """The RCCL pieces on one rank: a world-1 communicator, the metric all-reduce (= the local
     sum of the episode rewards) and the table fingerprint all-gather (changes when the table does)."""

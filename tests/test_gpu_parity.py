@@ -156,6 +156,29 @@ def test_philox_matches_oracle_and_t0(placement):
     assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
 
 
+@pytest.mark.parametrize("placement,kernel", [("prepass", "auto"), ("inkernel", "auto"), ("inkernel", "general")])
+def test_small_epsilon_actions_from_their_own_block(placement, kernel):
+    """epsilon below 2^-8 (threshold < 2^24): an exploring lane's action comes from the TAG_ACTION
+    Philox block, independent of its explore test (w % 3 of a w below a small threshold
+    is biased).  Fast (pre-pass and in-kernel draws) and general kernels against the oracle."""
+    S, N, R, T = 512, 2, 1, 96
+    inp = scenario_batch(S, N, T, seed=13)
+    ob = _oracle_for(inp, N, R)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = _device_for(inp, N, R)
+    explored = 0
+    for e, eps in enumerate((0.003, 0.0009)):
+        eng.run_episode("train", "philox", episode=e, epsilon=eps, record=REC, philox=placement, kernel=kernel)
+        out = ob.run_episode("train", rng="philox", seed=42, episode=e, eps=eps)
+        _compare(out, eng.get_records(REC), (placement, kernel, e))
+        for t in range(T):
+            for r in range(R + 1):
+                u, _ = philox.decision_draws(42, e, np.arange(S * N), t, r, R, eps=eps)
+                explored += int((u < eps).sum())
+    assert explored > 100  # the small-epsilon branch did draw actions
+    assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
+
+
 def test_speculative_prepass_next_epsilon():
     """next_epsilon: the launch writes episode e+1's Philox codes at the caller's next epsilon
     (the decay schedule, community.py:279-286).  Right guesses (hits), wrong guesses (a recompute)
