@@ -252,10 +252,19 @@ def exchange_kind(args, world: int) -> str:
     return "host" if os.environ.get("P2PMG_BENCH_RANKS_SHARE_GPU") else "rccl"
 
 
-def rccl_comm(eng, rank: int, world: int, required: bool = False) -> str:
+def rccl_comm(eng, rank: int, world: int, required: bool = False, world1: bool = False) -> str:
     """The RCCL communicator of the rank's context (rank 0's unique id broadcast over gloo).
     Returns "" or the error; a rank without a communicator reports its metrics over gloo, so a
-    replicas-only workload still runs (required=True: the shared-state workloads need it)."""
+    replicas-only workload still runs (required=True: the shared-state workloads need it).
+    world1 (--rccl-world1): a one-rank communicator too, so the data-path collectives of the
+    multi-GPU code path run on one GPU (their cost without the xGMI transfer)."""
+    if world == 1 and world1 and not os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
+        from p2pmicrogrid_amd.engine import comm_unique_id
+        try:
+            eng.comm_init(comm_unique_id(), 0, 1)
+        except Exception as e:  # noqa: BLE001
+            return f"{type(e).__name__}: {e}"
+        return ""
     if world == 1:
         return ""
     from p2pmicrogrid_amd.distributed import broadcast_bytes
@@ -306,11 +315,11 @@ MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_16x
 DQN_FWD_FLOP = 2 * (5 * 64 + 64 * 64 + 64 * 1)  # QNetwork (rl.py:135-148): 8,960 FLOP per row
 
 
-def collective_record(eng, world: int, steps: int, kind: str = "RCCL allReduce (data path)"):
+def collective_record(eng, world: int, steps: int, kind: str = "RCCL allReduce (data path)", world1: bool = False):
     """The data-path collectives of the timed episodes (shared-table delta all-reduce once per
     episode, DQN gradient-segment all-gather once per env step): HIP-event time on the rank's
-    stream, every call counted, rank 0's view (world > 1)."""
-    if world <= 1 or not hasattr(eng, "collective_ms"):
+    stream, every call counted, rank 0's view (world > 1, or a --rccl-world1 communicator)."""
+    if (world <= 1 and not world1) or not hasattr(eng, "collective_ms"):
         return None
     total, n = eng.collective_ms()
     return {"kind": kind, "calls": n, "ms_total": total,
@@ -426,7 +435,7 @@ def main_dqn(args, rank, world, local, S, N, R, T):
         eng.set_grad_exchange(lambda rows: all_gather_rows(rows, rank, world), rank, world)
         comm_err = "host-rehearsal exchange (no RCCL communicator)"
     else:  # gradient-segment all-gather every env step + metrics over RCCL
-        comm_err = rccl_comm(eng, rank, world, required=True)
+        comm_err = rccl_comm(eng, rank, world, required=True, world1=args.rccl_world1)
     record = ("reward", "cost")
     eng.run_episode("fill", "philox", episode=0, epsilon=1.0, record=record)  # community.init_buffers
     eng.reset_temperatures_philox(1, 0.3)
@@ -452,7 +461,8 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     rank_times = all_gather_float(time.perf_counter() - t0, world)
     dt = max(rank_times)
     kms = eng.kernel_times()
-    coll = collective_record(eng, world, args.steps, "RCCL allGather of the gradient segments (data path)")
+    coll = collective_record(eng, world, args.steps, "RCCL allGather of the gradient segments (data path)",
+                             world1=args.rccl_world1 and not comm_err)
     # every rank's replica of the shared network (the same Adam step on the same gathered sum)
     from p2pmicrogrid_amd.distributed import all_gather_concat
     fps = all_gather_concat(np.array([weights_fingerprint(eng.get_weights("online"))], np.uint64), world)
@@ -710,7 +720,7 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
     if xk == "host":  # rehearsal: int64 deltas and metrics summed over gloo
         comm_err = "host-rehearsal exchange (no RCCL communicator)"
     else:
-        comm_err = rccl_comm(eng, rank, world, required=shared and args.exchange == "rccl")
+        comm_err = rccl_comm(eng, rank, world, required=shared and args.exchange == "rccl", world1=args.rccl_world1)
         if comm_err and shared:  # --exchange auto without a communicator: the labelled host exchange
             fallback, xk = comm_err, "host"
     record = ("reward", "cost")
@@ -723,7 +733,7 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
             if world > 1 and xk == "host":
                 from p2pmicrogrid_amd.distributed import all_reduce_int64
                 eng.set_q_delta(all_reduce_int64(eng.get_q_delta(), world))
-            elif world > 1:
+            elif world > 1 or (args.rccl_world1 and not comm_err):
                 eng.allreduce_q_delta()
             eng.apply_q_delta()
             eng.reset_temperatures_philox(e + 1, 0.3)  # agent.reset() at the end of train_episode
@@ -746,7 +756,7 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
     eng.set_timing_period(timing_period)
     dt, rank_times = timed(eng, world, lambda: episodes(warmup, warmup + steps))
     kms = eng.kernel_times()
-    coll = collective_record(eng, world, steps)
+    coll = collective_record(eng, world, steps, world1=args.rccl_world1 and not comm_err)
     ep_reward = metrics[0][0] / metrics[0][1]
     nranks = eng.comm_nranks() if not comm_err else 0
     if shared and xk == "host":  # every replica's fingerprint, gathered over gloo
@@ -930,6 +940,9 @@ def main():
                     help="config5: gradient segments of this rank (0 = one; > 1 takes the split fold -> exchange "
                          "-> Adam path even at world 1)")
     ap.add_argument("--agents-per-block", type=int, default=0, help="config5: agents per train workgroup (0 = auto)")
+    ap.add_argument("--rccl-world1", action="store_true",
+                    help="at --gpus 1: a one-rank RCCL communicator, so the shared-state workloads run their "
+                         "multi-GPU exchange path (delta all-reduce / gradient all-gather) on one GPU")
     ap.add_argument("--secondary", default="auto", choices=["auto", "none", "config3"],
                     help="a second workload measured by the same ranks after the first (auto: configs[2], the "
                          "shared-table workload with the int64 delta all-reduce, after the default config2)")

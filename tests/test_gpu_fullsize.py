@@ -130,6 +130,56 @@ def test_full_size_config5_dqn_per_agent_sampled_oracle():
     eng.close()
 
 
+def test_full_size_config5_shared_gradient_segments_against_oracle():
+    """The benched configs[4] shape (4096 x 2 agents, ONE shared network, 16 agents per train
+    workgroup) at its first training env step: the gradient segments the device hands to the exchange
+    (p2pmg_dqn_set_exchange) are compared bit for bit with oracle/dqn.train_block + fold_segments over
+    the same agents, batches rebuilt from the device's replay rings (get_buffer) with the Philox
+    sample draws.  64 segments of 128 agents: the train workgroups are the bench layout's (blocks of
+    16 agents never straddle a segment), two sampled segments are re-run by the oracle."""
+    from p2pmicrogrid_amd.dataset import scenario_batch
+    from p2pmicrogrid_amd.dqn import DeviceDQNBatch
+    from oracle import philox
+    S, N, R, T, G, APB = 4096, 2, 1, 96, 64, 16
+    inp = scenario_batch(S, N, T)
+    eng = DeviceDQNBatch(S, N, R, T, shared=True, init_seed=0, grad_segments=G, agents_per_block=APB)
+    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+    eng.set_profiles(inp.load_w, inp.pv_w)
+    eng.set_max_in(inp.max_in)
+    eng.set_temperatures(inp.t_in0, inp.t_m0)
+    assert eng.grad_layout() == {"segments": G, "agents_per_block": APB, "blocks": S * N // APB}
+    th0 = eng.get_weights("online")[0]
+    eng.run_episode("fill", "philox", episode=0, epsilon=1.0)
+    eng.reset_temperatures_philox(1, 0.3)
+    captured = []
+
+    def capture(rows):  # rows [2, G * stride]: this context's segments in row 0 (world 2: the split path)
+        if not captured:
+            captured.append(rows[0].copy())
+        rows[1] = 0.0
+
+    eng.set_grad_exchange(capture, 0, 2)
+    eng.run_episode("train", "philox", episode=1, epsilon=0.9)
+    eng.sync()
+    assert captured, "the exchange was not called"
+    stride = captured[0].size // G
+    segs = captured[0].reshape(G, stride)[:, :odqn.N_PARAMS]
+    assert np.all(np.isfinite(segs)) and np.any(segs != 0)
+    seg_agents = S * N // G
+    for g in (0, 37):
+        first = g * seg_agents
+        ring, added = eng.get_buffer(first, seg_agents)
+        assert np.all(added == T + T)  # 96 fill + 96 train transitions, no eviction (capacity 5000)
+        # step 0 of the training episode: 97 transitions (the fill + the step's own), deque = ring slots
+        idx = philox.sample_draws(42, 1, np.arange(first, first + seg_agents), 0, np.full(seg_agents, T + 1), 32)
+        b = ring[np.arange(seg_agents)[:, None], idx]  # [agents, 32, 10]
+        _, _, bps, blocks = odqn.block_layout(seg_agents, 1, APB)
+        partials, _ = odqn.train_block(th0, th0, b.reshape(bps, APB, 32, 10), 0.95)
+        want = odqn.fold_segments(partials, bps)[0]
+        assert np.array_equal(segs[g], want), f"segment {g}: max |diff| {np.abs(segs[g] - want).max()}"
+    eng.close()
+
+
 def test_full_size_config5_dqn_shared_network_properties(monkeypatch):
     """The benched configs[4] shape: engine a acts with the MFMA act kernel (16 agents per
     workgroup), engine b with the one-wave-per-agent kernel (P2PMG_DQN_ACT=wave, checked against the
