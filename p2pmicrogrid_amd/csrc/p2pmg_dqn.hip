@@ -1180,14 +1180,36 @@ __global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kerne
 
 // shared network over several segments / ranks: the segments' sum in global segment order, the mean
 // over every agent of every rank, clip, Adam, soft update (every rank computes the same values)
-__global__ void dqn_adam_shared_kernel(const DqnParams d) {
+// Latency, not bandwidth (4609 parameters): the Adam state and every segment's value are loaded
+// before the first add (one memory round trip instead of one per segment), then summed in order.
+constexpr int kAdamSegBatch = 16;
+__global__ __launch_bounds__(256) void dqn_adam_shared_kernel(const DqnParams d) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= kDqnParams) return;
-  float t = d.segs[k];
-  for (int g = 1; g < d.n_segs; ++g) t += d.segs[(size_t)g * kNetStride + k];
+  const float m0 = d.adam_m[k], v0 = d.adam_v[k], w0 = d.theta[k], tg0 = d.target[k];
+  const int n = d.n_segs;
+  float t;
+  if (n <= kAdamSegBatch) {
+    float sv[kAdamSegBatch];
+#pragma unroll
+    for (int g = 0; g < kAdamSegBatch; ++g) sv[g] = g < n ? d.segs[(size_t)g * kNetStride + k] : 0.0f;
+    t = sv[0];
+#pragma unroll
+    for (int g = 1; g < kAdamSegBatch; ++g) t = g < n ? t + sv[g] : t;  // segs 0 + 1 + ... + n-1, in order
+  } else {
+    t = d.segs[k];
+    for (int g = 1; g < n; ++g) t += d.segs[(size_t)g * kNetStride + k];
+  }
   float gk = t * d.inv_agents;
   if (k < kOffB1) gk = fminf(fmaxf(gk, -d.clip), d.clip);
-  adam_update(d, d.theta, d.target, d.adam_m, d.adam_v, k, gk, d.lr_t);
+  // adam_update's arithmetic on the preloaded state (Keras Adam, then Trainer._soft_update rl.py:335-354)
+  const float m = m0 + (gk - m0) * d.b1c;
+  const float v = v0 + (gk * gk - v0) * d.b2c;
+  const float w = w0 - (m * d.lr_t) / (sqrtf(v) + d.adam_eps);
+  d.adam_m[k] = m;
+  d.adam_v[k] = v;
+  d.theta[k] = w;
+  d.target[k] = d.tau_c * tg0 + d.tau * w;
 }
 
 // QNetwork.call on explicit rows (object API, rl.py:147-148): one thread per row

@@ -1754,7 +1754,9 @@ __device__ __forceinline__ bool in_range19(float x) {
 // a negative divisor q0 = -+0 and the last fma returns +0 for a = +0: not the IEEE -0; the division
 // fuzz test checks the positive-divisor domain.)  Both lanes round like the scalar fma.
 __device__ __forceinline__ pkf2 fdiv_core_pk(pkf2 a, pkf2 b, pkf2 y) {
-  const pkf2 q0 = a * y;
+  // q0 as two scalar multiplies: v_mul_f32 issues at 2.6 SIMD cycles, v_pk_mul_f32 at 6.6
+  // (profiles/r04_ubench_rate.jsonl); the FMAs stay packed (v_pk_fma_f32 6.8 < 2 x 3.8)
+  const pkf2 q0 = {a.x * y.x, a.y * y.y};
   const pkf2 r = __builtin_elementwise_fma(b, q0, -a);
   return __builtin_elementwise_fma(-r, y, q0);  // one correction, as fdiv_core
 }
