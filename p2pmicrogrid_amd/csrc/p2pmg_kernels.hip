@@ -1722,6 +1722,20 @@ hipError_t launch_fast_pair(const EpisodeParams& p, const uint2* pre, void* recs
   return hipErrorInvalidValue;
 }
 
+// __double2ll_rn(x) in two VALU ops while |x| < 2^51: y = x + 1.5 * 2^52 lies in [2^52, 2^53), where
+// the f64 spacing is 1, so the add IS the round-to-nearest-even, and the integer sits in y's
+// significand: int64 = bits(y) - bits(1.5 * 2^52), whose low word is 0 (only the high word changes,
+// no borrow).  Otherwise (a TD delta of 2^11 or more, wave-uniformly tested) the library conversion.
+__device__ __forceinline__ long long rne_ll(double x) {
+  if (__all(fabs(x) < 0x1p51)) {
+    const double y = x + 0x1.8p52;
+    const unsigned lo = (unsigned)__double2loint(y);
+    const unsigned hi = (unsigned)__double2hiint(y) - 0x43380000u;
+    return (long long)(((unsigned long long)hi << 32) | lo);
+  }
+  return __double2ll_rn(x);
+}
+
 // ----------------------------------------------------------------- the fast shared-table path (N = 16)
 typedef float pkf2 __attribute__((ext_vector_type(2)));
 // v with lane (16 k + J) set to +0 for every k: the diagonal of a 16-agent scenario whose agent i
@@ -1855,7 +1869,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   const uint32_t T32 = (uint32_t)T;
   const uint32_t t1 = T32 > 1 ? 1u : 0u;
   uint32_t t2 = (2u % T32);  // step t + 2 (mod T) of the loop's iteration t
-  const uint32_t e1o = t1 * env_step, f1o = t1 * A32;
+  const uint32_t f1o = t1 * A32;
   // records: FastRec rows, or only {reward, cost} as float2 when nothing else was requested
   // (8 B instead of 32 B of writes per agent-step); masked-off lanes write a dummy row.  Compile
   // time, as in the fast kernel: no store-count branch for the vmcnt bookkeeping to be pessimistic about
@@ -1866,8 +1880,6 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
   char* rec_ptr = rec_on ? reinterpret_cast<char*>(p.rec_pack) + (size_t)a * rec_bytes : rec_dummy;
   const size_t rec_step = rec_on ? A * rec_bytes : 0;
 
-  EnvRow e0 = load_env(envb);
-  EnvRow e1 = load_env(envb + e1o);
   const uint2 w0 = sqpb[0];
   uint2 w1 = sqpb[f1o];
   // step t's state: the balance and the time / balance part of the row offset come precomputed
@@ -1915,7 +1927,9 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
 
   for (int t = 0; t < T; ++t) {
     const uint32_t t1n = t + 1 == T ? 0u : (uint32_t)t + 1u;  // step t + 1 (mod T)
-    const EnvRow e2 = load_env(envb + t2 * env_step);
+    // step t's env row {t_out, prices} at the top of the step, not carried across the loop: its first
+    // use (the RC update) is half a step of this wave's issue away, which the SIMD's other waves fill
+    const EnvRow e0 = load_env(envb + (uint32_t)t * env_step);
     const uint2 w2 = sqpb[t2 * A32];
     const CodeWords cw1r = step_codes(p, codes_a, t1n * code_step, (int)t1n, a, W, !kPair);
     const float balw = st.bal * mi;
@@ -2064,7 +2078,7 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
         lds_double* tdp = (lds_double*)(uintptr_t)tdk_addr;
         const double k_alpha = tdp[0], k_gamma = tdp[1];
         const double d = k_alpha * (((double)rw + k_gamma * (double)max3(rowN)) - (double)qsa);
-        const long long dv = __double2ll_rn(d * kDeltaScale);
+        const long long dv = rne_ll(d * kDeltaScale);
 #if P2PMG_SQ_ABL == 1
         if (dv == 0x7123456789LL)  // timing-only ablation: no hash insert (never true in practice)
 #endif
@@ -2098,8 +2112,6 @@ __global__ __launch_bounds__(kWave * kSq16Waves, P2PMG_SQ16_OCC) void episode_sq
 
     tin = tin1;
     tm = tm1;
-    e0 = e1;
-    e1 = e2;
     w1 = w2;
     t2 = t2 + 1u == T32 ? 0u : t2 + 1u;
     st = st1;

@@ -7,7 +7,8 @@
 # usage: gpu_refresh.sh ROUND [A|B]  (e.g. r04 A: bench lines, microbenchmark, kernel stats;
 #        B: PMC + SQ passes)
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
-RND="${1:-r04}"
+RND="${1:-r05}"
+PO="--secondary none --schedule-episodes 0"  # config2 passes that profile the primary episode kernel only
 O="$R/gpurun_out/$RND"; mkdir -p "$O"
 PART="${2:-A}"
 run() {  # name timeout args...
@@ -16,8 +17,9 @@ run() {  # name timeout args...
   tail -c 300 "$O/$n.json"; echo
 }
 if [ "$PART" = A ]; then
-run c2 300 --steps 200 --warmup 10
-run c2n2 300 --gpus 2 --steps 200 --warmup 10 --no-cpu-baseline
+run c2 400 --gpus 1 --steps 20 --warmup 5          # the driver's default command (configs[1] + configs[2] secondary)
+run c2long 300 --steps 200 --warmup 10 $PO
+run c2n2 400 --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline
 run c3 400 --workload config3 --steps 10 --warmup 2
 run c4 500 --workload config4 --steps 3 --warmup 1
 run c5 400 --workload config5 --steps 10 --warmup 2
@@ -33,15 +35,15 @@ pmc() {  # name counters timeout args...
   timeout -s KILL "$to" rocprofv3 --pmc $c --kernel-trace -d "$O/pmc_${n}_${c%% *}" -o "${c%% *}" --output-format csv -- python3 "$R/bench.py" "$@" --no-cpu-baseline > "$O/pmc_${n}_${c%% *}.log" 2>&1 || { tail -20 "$O/pmc_${n}_${c%% *}.log"; exit 1; }
 }
 if [ "$PART" = A ]; then
-prof c2 300 --steps 30 --warmup 3
+prof c2 400 --gpus 1 --steps 20 --warmup 5
 prof c3 300 --workload config3 --steps 4 --warmup 1
 prof c4 500 --workload config4 --steps 2 --warmup 1
 prof c5 300 --workload config5 --steps 3 --warmup 1
 echo done A
 exit 0
 fi
-pmc c2 FETCH_SIZE 200 --steps 6 --warmup 1
-pmc c2 WRITE_SIZE 200 --steps 6 --warmup 1
+pmc c2 FETCH_SIZE 200 --steps 6 --warmup 1 $PO
+pmc c2 WRITE_SIZE 200 --steps 6 --warmup 1 $PO
 pmc c3 FETCH_SIZE 300 --workload config3 --steps 2 --warmup 1
 pmc c3 WRITE_SIZE 300 --workload config3 --steps 2 --warmup 1
 pmc c4 FETCH_SIZE 400 --workload config4 --steps 1 --warmup 1
@@ -54,7 +56,7 @@ for W in config2 config3; do
   ST=8; [ $W = config3 ] && ST=2
   for P in A B; do
     C=$PA; [ $P = B ] && C=$PB
-    timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace -d "$O/sq/${W}_$P" -o p --output-format csv -- python3 "$R/bench.py" --workload $W --steps $ST --warmup 1 --no-cpu-baseline > "$O/sq_${W}_$P.log" 2>&1 || { tail -20 "$O/sq_${W}_$P.log"; exit 1; }
+    timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace -d "$O/sq/${W}_$P" -o p --output-format csv -- python3 "$R/bench.py" --workload $W --steps $ST --warmup 1 --no-cpu-baseline $PO > "$O/sq_${W}_$P.log" 2>&1 || { tail -20 "$O/sq_${W}_$P.log"; exit 1; }
   done
 done
 # configs[4]: the DQN kernels' MFMA busy cycles beside the clock (SQ_BUSY_CYCLES) and the VALU / LDS
