@@ -446,6 +446,8 @@ def main_dqn(args, rank, world, local, S, N, R, T):
 
     for e in range(1, 1 + args.warmup):
         episode(e)
+    if world > 1 and args.warmup > 0:  # the first metric all-reduce sets up the communicator: not timed
+        episode_metrics(eng, world, comm_err)
     eng.sync()
     eng.reset_kernel_times()
     barrier(world)
@@ -749,6 +751,8 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
 
     for e in range(warmup):
         episode(e)
+    if world > 1 and warmup > 0:  # the first collective on a communicator sets up its connections: not timed
+        episode_metrics(eng, world, comm_err)
     eng.sync()
     eng.reset_kernel_times()
     # HIP events on every launch cost ~4 us per configs[1] episode: sample every 5th launch
