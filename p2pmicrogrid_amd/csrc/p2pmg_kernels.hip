@@ -1315,6 +1315,15 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
     }
     trMid = tr1;  // no candidate rows (N != 2 or a battery): "round1" runs from the rows' arrival
 #endif
+    double soc_r = soc;  // tentative SoC of the current round
+    BatPre bpre{};
+    if constexpr (BAT == 2) bpre = bat_pre(soc, bcap, bk);  // shared by the step's rounds
+    auto bat_rule = [&](float o, double& sr) -> float {
+      if constexpr (BAT == 2) return (float)battery_rule_pre((double)o, sr, rcap, bk, bpre);
+      return (float)battery_rule_r<true>((double)o, sr, bcap, rcap, bk);
+    };
+    // (round 0's rule for all 3 actions ahead of the rows' wait measured slower: configs[3] 57.1 ->
+    // 59.5 ms, profiles/r05_ab/bat_spec0_ab.txt)
     row0 = patched(row0, a0, pat);  // ... may have hit a prefetched row
 
     // round 0 (P = 0: every filtered power is -0, tot = 0, even split)
@@ -1383,13 +1392,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
       settle_next();
     }
     float out0 = balw + hp;
-    double soc_r = soc;  // tentative SoC of the current round
-    BatPre bpre{};
-    if constexpr (BAT == 2) bpre = bat_pre(soc, bcap, bk);  // shared by the step's rounds
-    auto bat_rule = [&](float o, double& sr) -> float {
-      if constexpr (BAT == 2) return (float)battery_rule_pre((double)o, sr, rcap, bk, bpre);
-      return (float)battery_rule_r<true>((double)o, sr, bcap, rcap, bk);
-    };
     if constexpr (BAT != 0) {
       if (bcap > 0.0) out0 = bat_rule(out0, soc_r);
     }
