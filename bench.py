@@ -588,14 +588,18 @@ SQ_ENGINES = 32          # shader engines whose SQ_BUSY_CYCLES rocprofv3 sums (8
 ONE_WAVE_PEAK_G = CLOCK_GHZ / 4
 
 
-def issue_roofline(workload: str, kernel_ms: float):
+def issue_roofline(workload: str, kernel_ms: float, sizes=None):
     """Instruction-issue roofline of the episode kernel: the VALU wave-instructions one launch
     issues (SQ_INSTS_VALU from the committed rocprofv3 counter pass, profiles/sq_<workload>.json,
     scripts/gpu_sq_counters.sh) over the live kernel time, against the chip's VALU issue peak and,
-    when every wave has a SIMD to itself, against that wave's own issue ceiling."""
+    when every wave has a SIMD to itself, against that wave's own issue ceiling.  The counter pass
+    ran the workload's default sizes: a run at other (scenarios, agents, rounds, horizon) gets no block."""
     path = os.path.join(ROOT, "profiles", f"sq_{workload}.json")
     if not os.path.exists(path) or not kernel_ms == kernel_ms:
         return None
+    if sizes is not None and workload in WORKLOADS:
+        if tuple(sizes) != tuple(WORKLOADS[workload][:4]):
+            return None
     try:
         d = json.load(open(path))
     except Exception:  # noqa: BLE001
@@ -873,7 +877,7 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
             sm = sector_model_per_agent_step(N, R, eps_mid, battery or hetero)
             sm["bytes_per_launch"] = sm["total"] * steps_per_episode
             out["roofline"]["sector_model"] = sm
-        issue = issue_roofline(wl, kernel_ms)
+        issue = issue_roofline(wl, kernel_ms, (S, N, R, T))
         if issue:
             out["roofline"]["issue"] = issue
         # What binds the kernel: achieved/peak/frac above stay the HBM roofline
