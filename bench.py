@@ -655,7 +655,7 @@ def gather_roofline(n_agents: int, horizon: int, kernel_ms: float, stages: int =
                 and d.get("stages", 1) == stages and d.get("agents_per_wave") == agents_per_wave
                 and not d.get("pair_lanes") and d.get("pool_rows") == pool):
             floor_us = d["kernel_us"]
-            return {"unit": "us per launch", "floor": floor_us, "achieved": kernel_ms * 1e3,
+            return {"unit": "us per episode", "floor": floor_us, "achieved": kernel_ms * 1e3,
                     "frac": floor_us / (kernel_ms * 1e3), "floor_cycles_per_step": d["cycles_per_step"],
                     "source": os.path.relpath(path, ROOT)}
     return None
@@ -674,6 +674,7 @@ def load_traffic(path: str, workload: str):
     return d
 
 
+MAX_CHAIN = 64  # episodes per chained launch (p2pmg.h p2pmg_run_episodes)
 REFERENCE_EPISODES = 1000  # setup.py:30 max_episodes: the reference's training run (community.py:272-298)
 
 
@@ -747,23 +748,56 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
             eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record, reset_sigma=0.3,
                             next_epsilon=epsilon_at(e + 1))
 
-    def episodes(e0, e1):
-        for k, e in enumerate(range(e0, e1)):
-            episode(e)
-            if (k + 1) % args.metric_every == 0 or e + 1 == e1:
-                metrics[0] = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
+    # per-agent tables: chained launches (p2pmg_run_episodes), each running the episodes up to the
+    # next metric point back to back in every wave; same results as one launch per episode
+    chain = not shared and args.chain == "auto"
+    launch_eps = []  # episodes of every launch since the last reset_kernel_times (chained mode)
 
-    for e in range(warmup):
-        episode(e)
+    def first_chain(e0, e1):  # the episodes of the first launch of episodes(e0, e1)
+        return min(e1, e0 + args.metric_every, e0 + MAX_CHAIN) - e0
+
+    def episodes(e0, e1, metric=True, next_end=None):
+        """Episodes [e0, e1) with the metric all-reduce every --metric-every episodes and after the
+        last; next_end: where the caller's next episodes(e1, next_end) ends (the pre-pass guess)."""
+        if not chain:
+            for k, e in enumerate(range(e0, e1)):
+                episode(e)
+                if metric and ((k + 1) % args.metric_every == 0 or e + 1 == e1):
+                    metrics[0] = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
+            return
+        k0 = e0
+        while k0 < e1:
+            k1 = k0 + first_chain(k0, e1)
+            n_next = first_chain(k1, e1) if k1 < e1 else (first_chain(e1, next_end) if next_end else k1 - k0)
+            eng.run_episodes(k0, [epsilon_at(e) for e in range(k0, k1)], reset_sigma=0.3, record=record,
+                             next_epsilons=[epsilon_at(e) for e in range(k1, k1 + n_next)])
+            launch_eps.append(k1 - k0)
+            if metric:
+                metrics[0] = episode_metrics(eng, world, comm_err)  # every chain ends at a metric point
+            k0 = k1
+
+    def kernel_ms_per_episode(kms):
+        """HIP-event kernel time per episode: chained launches cover launch_eps[i] episodes each."""
+        if not len(kms):
+            return None
+        if not chain:
+            return float(np.mean(kms))
+        return float(np.sum(kms)) / float(np.sum(launch_eps[-len(kms):]))
+
+    episodes(0, warmup, metric=False, next_end=warmup + steps)
     if world > 1 and warmup > 0:  # the first collective on a communicator sets up its connections: not timed
         episode_metrics(eng, world, comm_err)
     eng.sync()
     eng.reset_kernel_times()
-    # HIP events on every launch cost ~4 us per configs[1] episode: sample every 5th launch
-    timing_period = 5 if steps >= 20 else 1
+    launch_eps.clear()
+    # HIP events on every launch cost ~4 us per configs[1] episode: sample every 5th launch (every
+    # chained launch: one per metric period)
+    timing_period = 5 if steps >= 20 and not chain else 1
     eng.set_timing_period(timing_period)
-    dt, rank_times = timed(eng, world, lambda: episodes(warmup, warmup + steps))
+    nxt_end = min(schedule_to, warmup + steps + args.metric_every) if schedule_to > warmup + steps else None
+    dt, rank_times = timed(eng, world, lambda: episodes(warmup, warmup + steps, next_end=nxt_end))
     kms = eng.kernel_times()
+    kernel_ms_ep = kernel_ms_per_episode(kms)
     coll = collective_record(eng, world, steps, world1=args.rccl_world1 and not comm_err)
     ep_reward = metrics[0][0] / metrics[0][1]
     nranks = eng.comm_nranks() if not comm_err else 0
@@ -781,15 +815,16 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
         cur = warmup + steps
         t_all = 0.0
         for w0 in sorted(w for w in eps_windows if cur <= w and w + window_steps <= schedule_to):
-            dt_gap, _ = timed(eng, world, lambda: episodes(cur, w0))
+            dt_gap, _ = timed(eng, world, lambda: episodes(cur, w0, next_end=w0 + window_steps))
             eng.reset_kernel_times()
-            dt_w, _ = timed(eng, world, lambda: episodes(w0, w0 + window_steps))
+            launch_eps.clear()
+            dt_w, _ = timed(eng, world, lambda: episodes(w0, w0 + window_steps, next_end=schedule_to))
             kw_ = eng.kernel_times()
             at_eps["windows"].append({
                 "first_episode": w0, "episodes": window_steps, "epsilon": epsilon_at(w0),
                 "epsilon_last": epsilon_at(w0 + window_steps - 1),
                 "value": world * steps_per_episode * window_steps / dt_w, "ms_per_step": dt_w / window_steps * 1e3,
-                "kernel_ms": float(np.mean(kw_)) if len(kw_) else None, "timed_launches": int(len(kw_))})
+                "kernel_ms": kernel_ms_per_episode(kw_), "timed_launches": int(len(kw_))})
             t_all += dt_gap + dt_w
             cur = w0 + window_steps
         dt_tail, _ = timed(eng, world, lambda: episodes(cur, schedule_to))
@@ -821,7 +856,7 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
             bpa = algorithmic_bytes_per_agent_step(R, q_bytes, outputs=len(record))
             workload = (f"configs[1]: {S} scenarios/GPU x thesis community (N={N}, R={R}, T={T}), per-agent "
                         f"{q_dtype} Q-tables, Philox exploration, train episodes")
-        kernel_ms = float(np.mean(kms)) if len(kms) else float("nan")
+        kernel_ms = kernel_ms_ep if kernel_ms_ep is not None else float("nan")
         achieved = bpa * steps_per_episode / (kernel_ms * 1e-3) / 1e9
         tj = args.traffic_json if (args.traffic_json and wl == args.workload) else os.path.join(
             ROOT, "profiles", "pmc_traffic.json" if wl == "config2" else f"pmc_traffic_{wl}.json")
@@ -848,9 +883,13 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
                          "kernel": eng.last_kernel(),
-                         "kernel_ms": kernel_ms,
+                         "kernel_ms": kernel_ms,  # per episode (a chained launch runs several)
+                         "kernel_ms_per_launch": float(np.mean(kms)) if len(kms) else None,
+                         "episodes_per_launch": list(launch_eps) if chain else 1,
                          "algorithmic_bytes_per_agent_step": bpa,
-                         "algorithmic_bytes_per_launch": bpa * steps_per_episode,
+                         "algorithmic_bytes_per_episode": bpa * steps_per_episode,
+                         "algorithmic_bytes_per_launch": bpa * steps_per_episode * (
+                             float(np.mean(launch_eps)) if chain and launch_eps else 1.0),
                          "timed_launches": int(len(kms)), "timing_period": timing_period},
             "mean_episode_reward": ep_reward,
             "epsilon_range": [epsilon_at(warmup), epsilon_at(warmup + steps - 1)],
@@ -951,6 +990,9 @@ def main():
     ap.add_argument("--rccl-world1", action="store_true",
                     help="at --gpus 1: a one-rank RCCL communicator, so the shared-state workloads run their "
                          "multi-GPU exchange path (delta all-reduce / gradient all-gather) on one GPU")
+    ap.add_argument("--chain", default="auto", choices=["auto", "off"],
+                    help="per-agent tables: chained launches (p2pmg_run_episodes, every wave running the "
+                         "episodes up to the next metric point back to back) or one launch per episode")
     ap.add_argument("--secondary", default="auto", choices=["auto", "none", "config3"],
                     help="a second workload measured by the same ranks after the first (auto: configs[2], the "
                          "shared-table workload with the int64 delta all-reduce, after the default config2)")

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define P2PMG_ABI_VERSION 6  /* 3: p2pmg_episode_args.next_epsilon; 4: P2PMG_FLAG_NEXT_EPSILON, p2pmg_prepass_stats, per-network Adam steps; 5: p2pmg_collective_ms; 6: DQN gradient segments, p2pmg_dqn_set_exchange, p2pmg_dqn_grad_layout */
+#define P2PMG_ABI_VERSION 7  /* 3: p2pmg_episode_args.next_epsilon; 4: P2PMG_FLAG_NEXT_EPSILON, p2pmg_prepass_stats, per-network Adam steps; 5: p2pmg_collective_ms; 6: DQN gradient segments, p2pmg_dqn_set_exchange, p2pmg_dqn_grad_layout; 7: p2pmg_run_episodes, p2pmg_get_episode_rewards */
 
 typedef struct p2pmg_ctx p2pmg_ctx;
 
@@ -185,6 +185,18 @@ int p2pmg_get_q(p2pmg_ctx* ctx, int first_agent, int count, void* host, int host
 
 /* the hot path */
 int p2pmg_run_episode(p2pmg_ctx* ctx, const p2pmg_episode_args* args);
+/* n consecutive episodes: the loop body of CommunityMicrogrid's training loop (community.py:279-286,
+ * train_episode x n), episode args->episode + k at epsilons[k], every other field of args as in
+ * p2pmg_run_episode.  Training with Philox draws, where the fast kernel applies, runs as chained
+ * launches (up to 64 episodes per launch, every wave running its episodes back to back); anything
+ * else as n launches.  Results, tables, T0 resets and the records left behind (the last episode's)
+ * are those of the n p2pmg_run_episode calls, bit for bit.  next_n / next_epsilons: the caller's
+ * guess of the NEXT call's epsilons for the speculative pre-pass (as next_epsilon; next_n = 0: the
+ * same as this call's last).  p2pmg_get_episode_reward returns the last episode's reward. */
+int p2pmg_run_episodes(p2pmg_ctx* ctx, const p2pmg_episode_args* args, int n, const double* epsilons, int next_n,
+                       const double* next_epsilons);
+/* [n][S] episode rewards (community.py:179) of the first n episodes of the last p2pmg_run_episodes call */
+int p2pmg_get_episode_rewards(p2pmg_ctx* ctx, int n, float* host);
 /* one P2PMG_REC_* bit of the LAST episode launch; P2PMG_E_STATE if that launch did not record it */
 int p2pmg_get_record(p2pmg_ctx* ctx, int which, void* host);
 /* fast path: episode launches whose step pre-pass the previous launch had already produced (hits)

@@ -40,6 +40,7 @@ EXPORTS = [
     "p2pmg_dqn_set_buffer", "p2pmg_dqn_forward", "p2pmg_dqn_train_batch", "p2pmg_prepass_stats",
     "p2pmg_dqn_get_net_steps", "p2pmg_fdiv_check", "p2pmg_fdiv64_check", "p2pmg_comm_nranks",
     "p2pmg_allreduce_metrics", "p2pmg_table_hash_allgather", "p2pmg_dqn_set_exchange", "p2pmg_dqn_grad_layout",
+    "p2pmg_run_episodes", "p2pmg_get_episode_rewards",
 ]
 
 
@@ -64,7 +65,7 @@ class DqnConfig(C.Structure):
                 ("capacity", C.c_int32), ("agents_per_block", C.c_int32), ("grad_segments", C.c_int32)]
 
 
-ABI_VERSION = 6  # include/p2pmg.h P2PMG_ABI_VERSION
+ABI_VERSION = 7  # include/p2pmg.h P2PMG_ABI_VERSION
 
 # p2pmg_exchange_fn: int (*)(void* user, float* segments, int64_t floats_per_rank, int rank, int nranks)
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_int64, C.c_int, C.c_int)
@@ -91,6 +92,7 @@ P = C.c_void_p
 def _declare(lib):
     vp, i32, sz = C.c_void_p, C.c_int, C.c_size_t
     fp = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+    dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
     sig = {
         "p2pmg_abi_version": ([], i32),
         "p2pmg_config_default": ([C.POINTER(Config)], i32),
@@ -111,6 +113,8 @@ def _declare(lib):
         "p2pmg_set_q": ([vp, i32, i32, vp, i32], i32),
         "p2pmg_get_q": ([vp, i32, i32, vp, i32], i32),
         "p2pmg_run_episode": ([vp, C.POINTER(EpisodeArgs)], i32),
+        "p2pmg_run_episodes": ([vp, C.POINTER(EpisodeArgs), i32, dp, i32, vp], i32),
+        "p2pmg_get_episode_rewards": ([vp, i32, fp], i32),
         "p2pmg_get_record": ([vp, i32, vp], i32),
         "p2pmg_get_episode_reward": ([vp, fp], i32),
         "p2pmg_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i32),

@@ -61,6 +61,13 @@ struct EpisodeParams {
   int rec_narrow;            // fast / sq16: only reward + cost requested -> records are [T][A] float2
   int reset_t0;              // fast path: draw T0 for episode + 1 at the end (P2PMG_FLAG_RESET_T0)
   double reset_sigma;
+  // fast path, chained launch (p2pmg_run_episodes): `chain` consecutive training episodes
+  // (episode + k, k < chain) in one launch, each wave running them back to back; episode k reads
+  // its code words at codes + k * codes_stride and writes its episode reward to
+  // chain_rewards[k * S + s] (when non-null).  0 or 1: one episode.
+  int chain;
+  size_t codes_stride;
+  float* chain_rewards;
   int nt, nT, nb, np;
   double alpha, gamma;
   float hp_levels[4];
@@ -128,14 +135,21 @@ hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t strea
 // fast per-agent-table path: step pre-pass ([T][A] {balw, bins}; optionally the Philox code
 // words) + episode_fast_kernel (N <= 8, R + 1 <= 4, no battery, no shared table)
 // Where one step pre-pass writes: its buffers and the episode its Philox draws are for.
+constexpr int kMaxChain = 64;  // episodes per chained launch (their thresholds travel in the kernarg)
 struct PrepOut {
   uint2* pre;      // [T][A]
   uint32_t* ipc;   // [T][A] or null (N != 2)
-  uint32_t* words; // [T][W][A] or null (no Philox draws)
+  uint32_t* words; // [T][W][A] or null (no Philox draws); a chain: n_ep such buffers, words_stride apart
   int episode;
   double eps;      // the epsilon its Philox draws are for
   uint32_t eps_thr;  // its integer threshold (eps_threshold)
   int eps_all;
+  // a chain of n_ep > 1 episodes (episode + k): episode k's threshold ep_thr[k], all-explore bit k of
+  // ep_all (eps / eps_thr / eps_all unused)
+  int n_ep;
+  size_t words_stride;
+  uint32_t ep_thr[kMaxChain];
+  uint64_t ep_all;
 };
 // w / 2^32 < eps  <=>  w < ceil(eps * 2^32) for every 32-bit w (w / 2^32 and eps * 2^32 are exact in
 // f64): thr = that ceiling, clamped to [0, 2^32]; all = (thr == 2^32), when every w explores

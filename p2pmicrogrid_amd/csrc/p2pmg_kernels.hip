@@ -891,7 +891,9 @@ __device__ __forceinline__ void t0_draw(uint32_t k0, uint32_t k1, int episode, u
 //                 (row / np of the state (it, 0, ib, 0) and of the next state, rl.py:89-95;
 //                  the next state's balance is that of the next profile row, wrapping at T)
 // PHILOX = true also writes the step's exploration code words (philox_codes_kernel's job).
-__device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOut& o, size_t k) {
+// ep: the episode of a chain (o.n_ep > 1) whose code words to write; the policy-independent words
+// are the same for every episode and written with episode 0's.
+__device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOut& o, size_t k, int ep = 0) {
   const int t = (int)(k / p.A), a = (int)(k % p.A);
   const int tn = t + 1 == p.T ? 0 : t + 1;
   const int se = p.n_env == 1 ? 0 : a / p.N;
@@ -903,8 +905,8 @@ __device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOu
   const uint32_t tb = (uint32_t)(p.nT * p.nb);
   const uint32_t lo = (uint32_t)idx_time(time_t, p.nt) * tb + (uint32_t)idx_plain(bal, p.nb);
   const uint32_t hi = (uint32_t)idx_time(time_n, p.nt) * tb + (uint32_t)idx_plain(baln, p.nb);
-  o.pre[k] = make_uint2(__float_as_uint(bal * mi), lo | (hi << 16));
-  if (o.ipc) {
+  if (ep == 0) o.pre[k] = make_uint2(__float_as_uint(bal * mi), lo | (hi << 16));
+  if (o.ipc && ep == 0) {
     // N = 2: round 1's p2p feature depends only on the partner's round-0 action b (agent.py:203):
     // its column entry is ev_b = ((balw_p + hp_p[b]) * 1) / 2 (the even split of round 0), summed
     // as in the kernel's acc loop.  Byte b = the bin for b, so the kernel's round-1 rows can be
@@ -926,20 +928,22 @@ __device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOu
   }
   if (o.words) {
     EpisodeParams q = p;
-    q.episode = o.episode;
+    const bool chain = o.n_ep > 1;
+    q.episode = o.episode + ep;
     q.eps = o.eps;
-    q.eps_thr = o.eps_thr;
-    q.eps_all = o.eps_all;
+    q.eps_thr = chain ? o.ep_thr[ep] : o.eps_thr;
+    q.eps_all = chain ? (int)((o.ep_all >> ep) & 1u) : o.eps_all;
     const int R1 = p.R + 1, W = (R1 + 3) >> 2;
     const uint64_t codes = philox_codes_of(q, t, p.agent_offset + (uint32_t)a);
-    for (int w = 0; w < W; ++w) o.words[((size_t)t * W + w) * p.A + a] = (uint32_t)(codes >> (32 * w));
+    uint32_t* words = o.words + (size_t)ep * o.words_stride;
+    for (int w = 0; w < W; ++w) words[((size_t)t * W + w) * p.A + a] = (uint32_t)(codes >> (32 * w));
   }
 }
 #if P2PMG_IN_PART(0)
 __global__ void step_prepass_kernel(const EpisodeParams p, const PrepOut o) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // k = t * A + a
   if (k >= (size_t)p.T * p.A) return;
-  prepass_one(p, o, k);
+  prepass_one(p, o, k, (int)blockIdx.y);  // blockIdx.y: the chain's episode (uniform per workgroup)
 }
 #endif
 
@@ -1138,7 +1142,10 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   // next launch needs neither a pre-pass launch nor a cross-stream wait.
   if ((int)blockIdx.x >= n_cons) {
     const size_t n = (size_t)p.T * p.A, stride = (size_t)(gridDim.x - n_cons) * kWave;
-    for (size_t k2 = (size_t)(blockIdx.x - n_cons) * kWave + threadIdx.x; k2 < n; k2 += stride) prepass_one(p, nxt, k2);
+    const int n_ep = nxt.n_ep > 1 ? nxt.n_ep : 1;  // the next launch's chain
+    for (int ep = 0; ep < n_ep; ++ep)
+      for (size_t k2 = (size_t)(blockIdx.x - n_cons) * kWave + threadIdx.x; k2 < n; k2 += stride)
+        prepass_one(p, nxt, k2, ep);
     return;
   }
   constexpr int G = pow2ceil(N);
@@ -1202,7 +1209,6 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const size_t rec_bytes = narrow ? sizeof(float2) : sizeof(FastRec);
   char* const rec_dummy = reinterpret_cast<char*>(reinterpret_cast<FastRec*>(p.dummy) + kWave + lane);
   const bool rec_on = p.record != 0 && active;
-  char* rec_ptr = rec_on ? reinterpret_cast<char*>(recs) + (size_t)a * rec_bytes : rec_dummy;
   const size_t rec_step = rec_on ? A * rec_bytes : 0;
 
   // idx_temp((T_in - setpoint) / margin) heating.py:118-120, rl.py:93; the launcher sends this
@@ -1216,420 +1222,440 @@ __global__ __launch_bounds__(kWave) void episode_fast_kernel(const EpisodeParams
   const float* envb = p.env + (size_t)s_env * kEnvStride;
   const size_t env_step = (size_t)p.n_env * kEnvStride;
   const uint2* preb = pre + a;
-  const uint32_t* codes_a = p.codes + a;
   const uint32_t* ipc_a = p.pre_ipc + a;  // read only when CAND
   const int t1 = T > 1 ? 1 : 0, t2 = 2 % T;
-  // The per-step inputs (env row, pre-pass word, code word, round-1 bins) are fresh HBM lines every
-  // step, loaded three steps ahead into a 3-slot ring: slot t % 3 holds step t's, and step t
-  // refills its own slot with step t + 3's once those are dead.  The step loop is unrolled by three,
-  // so every slot is a fixed register set (no copies at the back edge, which would wait for the
-  // loads), and the refills are issued after the step's row gathers: loads complete in issue order,
-  // so a stream load issued ahead of the gathers would hold up the wait for them.
-  // Running (uniform, 32-bit) offsets of step t + 3, wrapping at T: T * A < 2^32 on this path.
-  const uint32_t TA = (uint32_t)T * (uint32_t)A, env_st = (uint32_t)env_step, env_end = env_st * (uint32_t)T;
-  uint32_t o3 = (uint32_t)(3 % T) * (uint32_t)A, eo3 = (uint32_t)(3 % T) * env_st;
+  // A chained launch runs p.chain episodes back to back in every wave (no launch boundary between
+  // them, and each wave starts its next episode as soon as its own ends): T_in / T_m carry over
+  // in registers (with the end-of-episode T0 reset when requested), the Q rows through memory.
+  const int n_chain = p.chain > 1 ? p.chain : 1;
+  for (int ep = 0; ep < n_chain; ++ep) {
+    const uint32_t* codes_a = p.codes + (size_t)ep * p.codes_stride + a;
+    char* rec_ptr = rec_on ? reinterpret_cast<char*>(recs) + (size_t)a * rec_bytes : rec_dummy;
+    // The per-step inputs (env row, pre-pass word, code word, round-1 bins) are fresh HBM lines every
+    // step, loaded three steps ahead into a 3-slot ring: slot t % 3 holds step t's, and step t
+    // refills its own slot with step t + 3's once those are dead.  The step loop is unrolled by three,
+    // so every slot is a fixed register set (no copies at the back edge, which would wait for the
+    // loads), and the refills are issued after the step's row gathers: loads complete in issue order,
+    // so a stream load issued ahead of the gathers would hold up the wait for them.
+    // Running (uniform, 32-bit) offsets of step t + 3, wrapping at T: T * A < 2^32 on this path.
+    const uint32_t TA = (uint32_t)T * (uint32_t)A, env_st = (uint32_t)env_step, env_end = env_st * (uint32_t)T;
+    uint32_t o3 = (uint32_t)(3 % T) * (uint32_t)A, eo3 = (uint32_t)(3 % T) * env_st;
 
-  // ring slots as vector values, so each stays one register tuple (a 16-B load's destination)
-  EnvV eS[3] = {load_envv(envb), load_envv(envb + (size_t)t1 * env_step), load_envv(envb + (size_t)t2 * env_step)};
-  uint2 pS[3] = {preb[0], preb[(size_t)t1 * A], preb[(size_t)t2 * A]};
-  uint32_t cS[3] = {codes_a[0], codes_a[(size_t)t1 * A], codes_a[(size_t)t2 * A]};
-  // masked-off lanes may explore too: they read agent 0's rows and store only to the dummy slots
-  auto code_of = [&](uint32_t w) { return TRAIN ? w : 0xFFFFFFFFu; };
-  uint32_t cw = code_of(cS[0]);
-  int iT = temp_bin(tin);
-  // row arithmetic in 24-bit multiplies (full-rate v_mul_u32_u24; every operand < 2^24)
-  auto strip_of = [&](uint32_t base, int it_) { return __umul24(base + __umul24((uint32_t)it_, (uint32_t)nbv), (uint32_t)np); };
-  uint32_t strip = strip_of(pS[0].y & 0xFFFFu, iT);
-  uint32_t nrow = strip_of(pS[0].y >> 16, iT) + (uint32_t)ip_zero;
-  auto row0_addr = [&](uint32_t st, uint32_t nr, uint32_t c) -> uint32_t {
-    const bool need = ((c & 0xFF) == 255) || (TRAIN && R1 == 1);  // greedy, or the TD target itself
-    return need ? st + (uint32_t)ip_zero : nr;
-  };
-  uint32_t a0 = row0_addr(strip, nrow, cw);
-  uint32_t aN = TRAIN ? nrow : a0;
-  Row4<QT> row0 = gat(a0);
-  Row4<QT> rowN = gat(aN);
-  uint32_t iS[3] = {0u, 0u, 0u};
-  Row4<QT> cand[3];
-  if constexpr (CAND) {
-    iS[0] = ipc_a[0];
-    iS[1] = ipc_a[(size_t)t1 * A];
-    iS[2] = ipc_a[(size_t)t2 * A];
+    // ring slots as vector values, so each stays one register tuple (a 16-B load's destination)
+    EnvV eS[3] = {load_envv(envb), load_envv(envb + (size_t)t1 * env_step), load_envv(envb + (size_t)t2 * env_step)};
+    uint2 pS[3] = {preb[0], preb[(size_t)t1 * A], preb[(size_t)t2 * A]};
+    uint32_t cS[3] = {codes_a[0], codes_a[(size_t)t1 * A], codes_a[(size_t)t2 * A]};
+    // masked-off lanes may explore too: they read agent 0's rows and store only to the dummy slots
+    auto code_of = [&](uint32_t w) { return TRAIN ? w : 0xFFFFFFFFu; };
+    uint32_t cw = code_of(cS[0]);
+    int iT = temp_bin(tin);
+    // row arithmetic in 24-bit multiplies (full-rate v_mul_u32_u24; every operand < 2^24)
+    auto strip_of = [&](uint32_t base, int it_) { return __umul24(base + __umul24((uint32_t)it_, (uint32_t)nbv), (uint32_t)np); };
+    uint32_t strip = strip_of(pS[0].y & 0xFFFFu, iT);
+    uint32_t nrow = strip_of(pS[0].y >> 16, iT) + (uint32_t)ip_zero;
+    auto row0_addr = [&](uint32_t st, uint32_t nr, uint32_t c) -> uint32_t {
+      const bool need = ((c & 0xFF) == 255) || (TRAIN && R1 == 1);  // greedy, or the TD target itself
+      return need ? st + (uint32_t)ip_zero : nr;
+    };
+    uint32_t a0 = row0_addr(strip, nrow, cw);
+    uint32_t aN = TRAIN ? nrow : a0;
+    Row4<QT> row0 = gat(a0);
+    Row4<QT> rowN = gat(aN);
+    uint32_t iS[3] = {0u, 0u, 0u};
+    Row4<QT> cand[3];
+    if constexpr (CAND) {
+      iS[0] = ipc_a[0];
+      iS[1] = ipc_a[(size_t)t1 * A];
+      iS[2] = ipc_a[(size_t)t2 * A];
 #pragma unroll
-    for (int b = 0; b < 3; ++b) cand[b] = gat((strip + ((iS[0] >> (8 * b)) & 0xFFu)));
-  }
-  Patch<QT> pat{0xFFFFFFFFu, 0, (QT)0};
-  float ep_sum = 0.0f;
+      for (int b = 0; b < 3; ++b) cand[b] = gat((strip + ((iS[0] >> (8 * b)) & 0xFFu)));
+    }
+    Patch<QT> pat{0xFFFFFFFFu, 0, (QT)0};
+    float ep_sum = 0.0f;
+    // the end-of-episode T0 reset depends only on (seed, episode + 1, agent): drawn here, while the
+    // first rows are in flight, and applied at the end (the f64 transcendentals off the episode tail)
+    float t0_in = tin, t0_m = tm;
+    if (p.reset_t0 && active)
+      t0_draw(p.seed_lo, p.seed_hi, p.episode + ep + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, t0_in,
+              t0_m);
 #if P2PMG_TRACE  // timing-only probe: per-step s_memtime splits of one wave, printed at the end
-  uint64_t trW = 0, trC = 0, trR = 0, trLast = 0, trA0 = 0, trWC = 0, trA1 = 0, trMid = 0, trCal = 0;
+    uint64_t trW = 0, trC = 0, trR = 0, trLast = 0, trA0 = 0, trWC = 0, trA1 = 0, trMid = 0, trCal = 0;
 #define P2PMG_STAMP(v) asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
 #endif
-  __builtin_amdgcn_s_waitcnt(0);  // enter the loop with nothing in flight (static waits inside)
+    __builtin_amdgcn_s_waitcnt(0);  // enter the loop with nothing in flight (static waits inside)
 
-  // one step; the loop below runs it three times per iteration (a manual unroll: the DPP exchanges
-  // are convergent, so the compiler will not unroll a loop with a runtime trip count): the input
-  // ring's slots and the prefetched rows' alternating registers stay put
-  auto step = [&](auto par) __attribute__((always_inline)) {
-    constexpr int P = decltype(par)::value, P1 = (P + 1) % 3;  // slots of step t and of step t + 1
-    const EnvV ev = eS[P];
-    const EnvRow e0{0.0f, ev.x, ev.y, ev.z, ev.w};
-    const uint2 p0 = pS[P], p1 = pS[P1];
-    const uint32_t c1 = cS[P1], ipc0 = iS[P], ipc1 = iS[P1];
-    const float balw = __uint_as_float(p0.x);
-    float row[N];
-    float col[N];
+    // one step; the loop below runs it three times per iteration (a manual unroll: the DPP exchanges
+    // are convergent, so the compiler will not unroll a loop with a runtime trip count): the input
+    // ring's slots and the prefetched rows' alternating registers stay put
+    auto step = [&](auto par) __attribute__((always_inline)) {
+      constexpr int P = decltype(par)::value, P1 = (P + 1) % 3;  // slots of step t and of step t + 1
+      const EnvV ev = eS[P];
+      const EnvRow e0{0.0f, ev.x, ev.y, ev.z, ev.w};
+      const uint2 p0 = pS[P], p1 = pS[P1];
+      const uint32_t c1 = cS[P1], ipc0 = iS[P], ipc1 = iS[P1];
+      const float balw = __uint_as_float(p0.x);
+      float row[N];
+      float col[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) { row[j] = 0.0f; col[j] = 0.0f; }
-    // the next step's T_in, temperature bin and table strips for each of the 3 actions
-    // (heating.py:37-56, rl.py:93): they need only this step's state, so they run while the rows
-    // are in flight, and the final action then merely selects one set (issue_next)
-    float tinA[3];
-    uint32_t iTA[3], stA[3], nrA[3];
-    {
-      const float ain = k.inv_ri * (tm - tin) + k.inv_rvent * (e0.t_out - tin);
-#pragma unroll
-      for (int x = 0; x < 3; ++x) {
-        const float d_in = k.inv_ci * (ain + hin[x]);
-        tinA[x] = tin + (d_in * k.spm) * k.slot;
-        iTA[x] = (uint32_t)temp_bin(tinA[x]);
-        stA[x] = strip_of(p1.y & 0xFFFFu, (int)iTA[x]);
-        nrA[x] = strip_of(p1.y >> 16, (int)iTA[x]) + (uint32_t)ip_zero;
-      }
-    }
-    // Between the rows' arrival and the next step's gathers the wave issues on the critical path
-    // (the gathers' latency is the rest of the step): only what those addresses need goes there;
-    // the TD target row's patch, T_m, the records and the market wait until the gathers are out.
-    const Patch<QT> pprev = pat;    // the previous step's TD store
-#if P2PMG_TRACE
-    uint64_t tr0, tr1;
-    P2PMG_STAMP(tr0);
-    if (trLast) trR += tr0 - trLast;
-    asm volatile("" ::"v"(row0.v[0]), "v"(row0.v[1]), "v"(row0.v[2]));
-    P2PMG_STAMP(tr1);
-    trW += tr1 - tr0;
-    {  // calibration: the cost of one stamp (two back to back)
-      uint64_t tcal;
-      P2PMG_STAMP(tcal);
-      trCal += tcal - tr1;
-      tr1 = tcal;
-    }
-    trMid = tr1;  // no candidate rows (N != 2 or a battery): "round1" runs from the rows' arrival
-#endif
-    double soc_r = soc;  // tentative SoC of the current round
-    BatPre bpre{};
-    if constexpr (BAT == 2) bpre = bat_pre(soc, bcap, bk);  // shared by the step's rounds
-    auto bat_rule = [&](float o, double& sr) -> float {
-      if constexpr (BAT == 2) return (float)battery_rule_pre((double)o, sr, rcap, bk, bpre);
-      return (float)battery_rule_r<true>((double)o, sr, bcap, rcap, bk);
-    };
-    // (round 0's rule for all 3 actions ahead of the rows' wait measured slower: configs[3] 57.1 ->
-    // 59.5 ms, profiles/r05_ab/bat_spec0_ab.txt)
-    row0 = patched(row0, a0, pat);  // ... may have hit a prefetched row
-
-    // round 0 (P = 0: every filtered power is -0, tot = 0, even split)
-    int code = (int)(cw & 0xFF);
-    int act = code == 255 ? argmax3(row0) : code;
-    float hp = hp_of(lv, act);
-    int ip = ip_zero;
-    Row4<QT> rowR = row0;
-    uint32_t acts = (uint32_t)act, ips = (uint32_t)ip_zero;
-    // CommunityMicrogrid._step -> HPHeating.step (community.py:184-188, heating.py:138-143) needs
-    // only the final round's heat-pump power: it and the next step's row gathers are issued as soon
-    // as that is known, ahead of the final round's divide-power and this step's market work
-    float tin1 = tin, tm1 = tm;
-    int iT1 = 0;
-    uint32_t strip1 = 0, cw1 = 0, a0n = 0, aNn = 0;
-    Row4<QT> row0n, rowNn, candn[3];
-    Sel3M mnext{};
-    auto issue_next = [&](int act_final) {
-      const Sel3M m = sel3_masks(act_final);
-      mnext = m;
-      strip1 = __float_as_uint(sel3(m, __uint_as_float(stA[0]), __uint_as_float(stA[1]), __uint_as_float(stA[2])));
-      const uint32_t nrow1 =
-          __float_as_uint(sel3(m, __uint_as_float(nrA[0]), __uint_as_float(nrA[1]), __uint_as_float(nrA[2])));
-      cw1 = code_of(c1);
-      a0n = row0_addr(strip1, nrow1, cw1);
-      aNn = TRAIN ? nrow1 : a0n;
-#if P2PMG_ABLATE == 8 || P2PMG_ABLATE == 10
-      row0n = fake_row(q + a0n * kQPad);
-      rowNn = fake_row(q + aNn * kQPad);
-#else
-      // the rows round 0 and round 1 wait for first, the TD's next-state row last.  Round 0's row
-      // only for the lanes that read it (a greedy round 0, or the TD target at R = 0): an exploring
-      // lane's gather would be address work in the CU's memory pipeline for nothing (an exec-masked
-      // load; configs[1] 79.8 -> 79.0 us, configs[3] 66.2 -> 65.3 ms at the bench's epsilon)
+      for (int j = 0; j < N; ++j) { row[j] = 0.0f; col[j] = 0.0f; }
+      // the next step's T_in, temperature bin and table strips for each of the 3 actions
+      // (heating.py:37-56, rl.py:93): they need only this step's state, so they run while the rows
+      // are in flight, and the final action then merely selects one set (issue_next)
+      float tinA[3];
+      uint32_t iTA[3], stA[3], nrA[3];
       {
-        Row4<QT> r0{};
-        if (((cw1 & 0xFF) == 255) || (TRAIN && R1 == 1)) r0 = gat(a0n);
-        row0n = r0;
-      }
-#endif
-      if constexpr (CAND) {
+        const float ain = k.inv_ri * (tm - tin) + k.inv_rvent * (e0.t_out - tin);
 #pragma unroll
-        for (int b = 0; b < 3; ++b) candn[b] = gat((strip1 + ((ipc1 >> (8 * b)) & 0xFFu)));
-      }
-#if !(P2PMG_ABLATE == 8 || P2PMG_ABLATE == 10)
-      rowNn = gat(aNn);
-#endif
-    };
-    // step t + 3's code word and round-1 bins into this step's slots (dead since step t - 1 / round 1)
-    auto refill_words = [&]() {
-      cS[P] = codes_a[o3];
-      if constexpr (CAND) iS[P] = ipc_a[o3];
-    };
-    // the rest of HPHeating.step for the chosen level, once the gathers are out
-    auto settle_next = [&]() {
-      const Sel3M& m = mnext;
-      iT1 = (int)__float_as_uint(sel3(m, __uint_as_float(iTA[0]), __uint_as_float(iTA[1]), __uint_as_float(iTA[2])));
-      tin1 = sel3(m, tinA[0], tinA[1], tinA[2]);
-      const float d_m = k.inv_cm * (((k.inv_ri * (tin - tm) + k.inv_re * (e0.t_out - tm)) + k.solar) +
-                                    sel3(m, hm[0], hm[1], hm[2]));  // heating.py:45,48
-      tm1 = tm + (d_m * k.spm) * k.slot;
-    };
-    if constexpr (R1 == 1) {
-      issue_next(act);
-      refill_words();
-      settle_next();
-    }
-    float out0 = balw + hp;
-    if constexpr (BAT != 0) {
-      if (bcap > 0.0) out0 = bat_rule(out0, soc_r);
-    }
-    const float ev0 = div_n_r<N>(out0 * 1.0f, rn);
-#pragma unroll
-    for (int j = 0; j < N; ++j) row[j] = ev0;
-#pragma unroll
-    for (int r = 1; r < R1; ++r) {
-      if (r == 1) {
-        gather_even<N, 1, G>(ev0, col, i);
-      } else {
-        exchange<N>(row, col, i, sl, nullptr);
-      }
-      code = (int)((cw >> (8 * r)) & 0xFF);
-      if (CAND && r == 1) {
-        // the partner's round-0 action picks the prefetched row (its bin is byte b of ipc0)
-        const int b = __float_as_int(shfl_xor_c<1>(__int_as_float(act)));
-#if P2PMG_TRACE
-        {
-          uint64_t ta, tb;
-          asm volatile("" ::"v"(b));
-          P2PMG_STAMP(ta);
-          asm volatile("" ::"v"(cand[0].v[0]), "v"(cand[1].v[0]), "v"(cand[2].v[0]), "v"(cand[0].v[2]), "v"(cand[1].v[2]),
-                       "v"(cand[2].v[2]));
-          P2PMG_STAMP(tb);
-          trA0 += ta - tr1;
-          trWC += tb - ta;
-          trMid = tb;
+        for (int x = 0; x < 3; ++x) {
+          const float d_in = k.inv_ci * (ain + hin[x]);
+          tinA[x] = tin + (d_in * k.spm) * k.slot;
+          iTA[x] = (uint32_t)temp_bin(tinA[x]);
+          stA[x] = strip_of(p1.y & 0xFFFFu, (int)iTA[x]);
+          nrA[x] = strip_of(p1.y >> 16, (int)iTA[x]) + (uint32_t)ip_zero;
         }
+      }
+      // Between the rows' arrival and the next step's gathers the wave issues on the critical path
+      // (the gathers' latency is the rest of the step): only what those addresses need goes there;
+      // the TD target row's patch, T_m, the records and the market wait until the gathers are out.
+      const Patch<QT> pprev = pat;    // the previous step's TD store
+#if P2PMG_TRACE
+      uint64_t tr0, tr1;
+      P2PMG_STAMP(tr0);
+      if (trLast) trR += tr0 - trLast;
+      asm volatile("" ::"v"(row0.v[0]), "v"(row0.v[1]), "v"(row0.v[2]));
+      P2PMG_STAMP(tr1);
+      trW += tr1 - tr0;
+      {  // calibration: the cost of one stamp (two back to back)
+        uint64_t tcal;
+        P2PMG_STAMP(tcal);
+        trCal += tcal - tr1;
+        tr1 = tcal;
+      }
+      trMid = tr1;  // no candidate rows (N != 2 or a battery): "round1" runs from the rows' arrival
 #endif
-        ip = (int)((ipc0 >> (8 * b)) & 0xFFu);
-        rowR = patched(sel_row(b, cand[0], cand[1], cand[2]), strip + (uint32_t)ip, pat);
-      } else {
-        float acc = 0.0f;
-#pragma unroll
-        for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : col[j]));
-        ip = p2p_bin(fdiv_b(div_n_r<N>(acc, rn), rmi));
-        const bool need = code == 255 || (TRAIN && r == R1 - 1);
-#if P2PMG_ABLATE == 7
-        rowR = fake_row(q + (need ? strip + (uint32_t)ip : a0) * kQPad);
+      double soc_r = soc;  // tentative SoC of the current round
+      BatPre bpre{};
+      if constexpr (BAT == 2) bpre = bat_pre(soc, bcap, bk);  // shared by the step's rounds
+      auto bat_rule = [&](float o, double& sr) -> float {
+        if constexpr (BAT == 2) return (float)battery_rule_pre((double)o, sr, rcap, bk, bpre);
+        return (float)battery_rule_r<true>((double)o, sr, bcap, rcap, bk);
+      };
+      // (round 0's rule for all 3 actions ahead of the rows' wait measured slower: configs[3] 57.1 ->
+      // 59.5 ms, profiles/r05_ab/bat_spec0_ab.txt)
+      row0 = patched(row0, a0, pat);  // ... may have hit a prefetched row
+
+      // round 0 (P = 0: every filtered power is -0, tot = 0, even split)
+      int code = (int)(cw & 0xFF);
+      int act = code == 255 ? argmax3(row0) : code;
+      float hp = hp_of(lv, act);
+      int ip = ip_zero;
+      Row4<QT> rowR = row0;
+      uint32_t acts = (uint32_t)act, ips = (uint32_t)ip_zero;
+      // CommunityMicrogrid._step -> HPHeating.step (community.py:184-188, heating.py:138-143) needs
+      // only the final round's heat-pump power: it and the next step's row gathers are issued as soon
+      // as that is known, ahead of the final round's divide-power and this step's market work
+      float tin1 = tin, tm1 = tm;
+      int iT1 = 0;
+      uint32_t strip1 = 0, cw1 = 0, a0n = 0, aNn = 0;
+      Row4<QT> row0n, rowNn, candn[3];
+      Sel3M mnext{};
+      auto issue_next = [&](int act_final) {
+        const Sel3M m = sel3_masks(act_final);
+        mnext = m;
+        strip1 = __float_as_uint(sel3(m, __uint_as_float(stA[0]), __uint_as_float(stA[1]), __uint_as_float(stA[2])));
+        const uint32_t nrow1 =
+            __float_as_uint(sel3(m, __uint_as_float(nrA[0]), __uint_as_float(nrA[1]), __uint_as_float(nrA[2])));
+        cw1 = code_of(c1);
+        a0n = row0_addr(strip1, nrow1, cw1);
+        aNn = TRAIN ? nrow1 : a0n;
+#if P2PMG_ABLATE == 8 || P2PMG_ABLATE == 10
+        row0n = fake_row(q + a0n * kQPad);
+        rowNn = fake_row(q + aNn * kQPad);
 #else
-        rowR = gat((need ? strip + (uint32_t)ip : a0));
-#endif
-      }
-#if P2PMG_BAT_SPEC
-      // the final round's battery rule for each of the 3 actions while its row is in flight (it
-      // needs only balw, the level and this step's SoC): the action then only selects
-      float outA[3];
-      double socA[3];
-      if constexpr (BAT != 0) {
-        if (r == R1 - 1) {
-#pragma unroll
-          for (int x = 0; x < 3; ++x) {
-            socA[x] = soc;
-            outA[x] = balw + hp_of(lv, x);
-            if (bcap > 0.0) outA[x] = bat_rule(outA[x], socA[x]);
-          }
-        }
-      }
-#endif
-      act = code == 255 ? argmax3(rowR) : code;
-      acts |= (uint32_t)act << (8 * r);
-      ips |= (uint32_t)ip << (8 * r);
-      hp = hp_of(lv, act);
-      if (r == R1 - 1) {
-#if P2PMG_TRACE
+        // the rows round 0 and round 1 wait for first, the TD's next-state row last.  Round 0's row
+        // only for the lanes that read it (a greedy round 0, or the TD target at R = 0): an exploring
+        // lane's gather would be address work in the CU's memory pipeline for nothing (an exec-masked
+        // load; configs[1] 79.8 -> 79.0 us, configs[3] 66.2 -> 65.3 ms at the bench's epsilon)
         {
-          uint64_t tc;
-          asm volatile("" ::"v"(act));
-          P2PMG_STAMP(tc);
-          trA1 += tc - trMid;
-          trMid = tc;
+          Row4<QT> r0{};
+          if (((cw1 & 0xFF) == 255) || (TRAIN && R1 == 1)) r0 = gat(a0n);
+          row0n = r0;
         }
 #endif
-        issue_next(act);
-#if P2PMG_TRACE
-        P2PMG_STAMP(trLast);
-        trC += trLast - trMid;
+        if constexpr (CAND) {
+#pragma unroll
+          for (int b = 0; b < 3; ++b) candn[b] = gat((strip1 + ((ipc1 >> (8 * b)) & 0xFFu)));
+        }
+#if !(P2PMG_ABLATE == 8 || P2PMG_ABLATE == 10)
+        rowNn = gat(aNn);
 #endif
+      };
+      // step t + 3's code word and round-1 bins into this step's slots (dead since step t - 1 / round 1)
+      auto refill_words = [&]() {
+        cS[P] = codes_a[o3];
+        if constexpr (CAND) iS[P] = ipc_a[o3];
+      };
+      // the rest of HPHeating.step for the chosen level, once the gathers are out
+      auto settle_next = [&]() {
+        const Sel3M& m = mnext;
+        iT1 = (int)__float_as_uint(sel3(m, __uint_as_float(iTA[0]), __uint_as_float(iTA[1]), __uint_as_float(iTA[2])));
+        tin1 = sel3(m, tinA[0], tinA[1], tinA[2]);
+        const float d_m = k.inv_cm * (((k.inv_ri * (tin - tm) + k.inv_re * (e0.t_out - tm)) + k.solar) +
+                                      sel3(m, hm[0], hm[1], hm[2]));  // heating.py:45,48
+        tm1 = tm + (d_m * k.spm) * k.slot;
+      };
+      if constexpr (R1 == 1) {
+        issue_next(act);
         refill_words();
         settle_next();
       }
-      float out = balw + hp;
+      float out0 = balw + hp;
       if constexpr (BAT != 0) {
-#if P2PMG_BAT_SPEC
-        if (r == R1 - 1) {
-          const Sel3M m = sel3_masks(act);
-          out = sel3(m, outA[0], outA[1], outA[2]);
-          soc_r = sel3(m, socA[0], socA[1], socA[2]);
-        } else
-#endif
-        {
-          soc_r = soc;
-          if (bcap > 0.0) out = bat_rule(out, soc_r);
+        if (bcap > 0.0) out0 = bat_rule(out0, soc_r);
+      }
+      const float ev0 = div_n_r<N>(out0 * 1.0f, rn);
+#pragma unroll
+      for (int j = 0; j < N; ++j) row[j] = ev0;
+#pragma unroll
+      for (int r = 1; r < R1; ++r) {
+        if (r == 1) {
+          gather_even<N, 1, G>(ev0, col, i);
+        } else {
+          exchange<N>(row, col, i, sl, nullptr);
         }
-      }
-#if P2PMG_ABLATE == 11  // timing-only: no final-round divide-power and no market (cost from out alone)
-      if (r == R1 - 1) {
-        row[0] = out;
-        continue;
-      }
-#endif
-      // _divide_power's filter keeps pw where sign(out) != sign(pw) (agent.py:187-188): for out > 0
-      // that is pw <= 0, for out < 0 pw >= 0, for out = 0 any pw.  A kept pw = +-0 and a dropped
-      // one (0) are interchangeable: every later use is |f| or a sum that already holds +0.
-      // As one clamp: f = med3(pw, out < 0 ? 0 : -inf, out > 0 ? 0 : +inf).
-      const float flo = out < 0.0f ? 0.0f : -__builtin_inff(), fhi = out > 0.0f ? 0.0f : __builtin_inff();
-      float f[N];
-      float tot = 0.0f;
-#pragma unroll
-      for (int j = 0; j < N; ++j) {
-        const float pw = -((j == i) ? 0.0f : col[j]);
-        f[j] = __builtin_amdgcn_fmed3f(pw, flo, fhi);
-        tot = tot + f[j];
-      }
-      tot = fabsf(tot);
-      const float ev = div_n_r<N>(out * 1.0f, rn);
-      // out * |f_j| / tot for every j: the diagonal's f_ii = +-0 gives out * 0 / tot = out * 0, the
-      // reference's value for it (agent.py:193-194), for any tot > 0.  One range guard per round.
-      const Recip rt = recip(tot == 0.0f ? 1.0f : tot);  // the tot = 0 lanes take ev
-      const float nout = nabs_out(out);
-      float num[N];
-      bool bad = !rt.ok;
-#pragma unroll
-      for (int j = 0; j < N; ++j) {
-        num[j] = nout * f[j];
-        row[j] = fdiv_core(num[j], rt);
-        bad = bad || !fdiv_ok(num[j]);
-      }
-      if (bad) {
-#pragma unroll
-        for (int j = 0; j < N; ++j) row[j] = fdiv_ieee(num[j], rt.b);
-      }
-#pragma unroll
-      for (int j = 0; j < N; ++j) row[j] = (tot == 0.0f) ? ev : row[j];
-    }
-    soc = soc_r;  // BatteryStorage state after the final round's decision
-    pat.row = 0xFFFFFFFFu;  // the next step's rows were issued after the previous TD store
-
-    // CommunityMicrogrid._assign_powers community.py:45-54 on the final P (diagonal kept)
-    float g = 0.0f, pp = 0.0f;
-#if P2PMG_ABLATE == 11
-    g = row[0];
-#else
-    exchange<N>(row, col, i, sl, nullptr);
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      // ex = sign(pij) * min(|pij|, |pji|) where the signs differ (community.py:48-50)
-      const float pij = row[j], pji = col[j];
-      const float ex = pair_exchange(pij, pji);
-      g = g + (pij - ex);
-      pp = pp + ex;
-    }
-#endif
-    // CommunityMicrogrid._compute_costs community.py:56-65
-    float cost = (g >= 0.0f) ? g * e0.buy : g * e0.inj;
-    cost = cost + pp * e0.p2p;
-    cost = fdiv_b(cost * k.slot, rmph);
-    cost = cost * k.kilo;
-    // RLAgent.get_reward agent.py:225-232 (pre-update T_in)
-    float pen = fmaxf(fmaxf(0.0f, k.lower - tin), fmaxf(0.0f, tin - k.upper));
-    pen = pen > 0.0f ? pen + 1.0f : 0.0f;
-    const float rw = -(cost + k.penw * pen);
-
-    if constexpr (TRAIN) {
-      // QAgent.train agent.py:293-298 -> QActor.train rl.py:119-129
-      const uint32_t srow = strip + (uint32_t)ip;
-      const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
-      const QT qnew = td_update(qsa, rw, max3(patched(rowN, aN, pprev)), k.alpha, k.gamma);
-      *(active ? q + srow * kQPad + act : q_dummy) = qnew;
-#if P2PMG_ABLATE == 9 || P2PMG_ABLATE == 10
-      pat = Patch<QT>{0xFFFFFFFFu, 0, (QT)0};  // timing-only: the next step does not wait for this TD
-#else
-      pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
-#endif
-    }
-    if constexpr (narrow) {
-      *reinterpret_cast<float2*>(__builtin_assume_aligned(rec_ptr, 8)) = make_float2(rw, cost);
-    } else {
-      const uint32_t bins = (p0.y & 0xFFFFu) | ((uint32_t)iT << 16);  // it * nT*nb + ib | iT << 16
-      float4* rp = reinterpret_cast<float4*>(__builtin_assume_aligned(rec_ptr, 16));
-      rp[0] = make_float4(rw, cost, g, pp);
-      rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
-    }
-    rec_ptr += rec_step;
-    // step t's env row and pre-pass word are dead: step t + 3's into their slots (the barrier keeps
-    // the scheduler from hoisting the loads above the old values' last use, which would need a
-    // second register set and a copy at the loop's back edge)
-    asm volatile("" ::: "memory");
-    eS[P] = load_envv(envb + eo3);
-    pS[P] = preb[o3];
-    // avg_reward = sum_t mean_i r (community.py:179), canonical sequential order
-    const float m = group_sum<N>(rw, lane, i, sl, nullptr);
-    ep_sum = ep_sum + div_n_r<N>(m, rn);
-
-    tin = tin1;
-    tm = tm1;
-    iT = iT1;
-    o3 += (uint32_t)A;
-    o3 = o3 == TA ? 0u : o3;
-    eo3 += env_st;
-    eo3 = eo3 == env_end ? 0u : eo3;
-    strip = strip1;
-    cw = cw1;
-    a0 = a0n;
-    aN = aNn;
-    row0 = row0n;
-    rowN = rowNn;
-    if constexpr (CAND) {
-#pragma unroll
-      for (int b = 0; b < 3; ++b) cand[b] = candn[b];
-    }
-  };
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-  using S2 = std::integral_constant<int, 2>;
-  int t = 0;
-  for (; t + 3 <= T; t += 3) {
-    step(S0{});
-    step(S1{});
-    step(S2{});
-  }
-  if (t < T) step(S0{});
-  if (t + 1 < T) step(S1{});
+        code = (int)((cw >> (8 * r)) & 0xFF);
+        if (CAND && r == 1) {
+          // the partner's round-0 action picks the prefetched row (its bin is byte b of ipc0)
+          const int b = __float_as_int(shfl_xor_c<1>(__int_as_float(act)));
 #if P2PMG_TRACE
-  if (threadIdx.x == 0 && (blockIdx.x == 0 || (int)blockIdx.x == n_cons / 2 || (int)blockIdx.x == n_cons - 1))
-    printf("TRACE blk %d/%d T %d: per step wait %.1f round0 %.1f waitcand %.1f round1 %.1f issue %.1f rest %.1f "
-           "(one stamp %.1f)\n",
-           (int)blockIdx.x, n_cons, T, (double)trW / T, (double)trA0 / T, (double)trWC / T, (double)trA1 / T,
-           (double)trC / T, (double)trR / (T - 1), (double)trCal / T);
+          {
+            uint64_t ta, tb;
+            asm volatile("" ::"v"(b));
+            P2PMG_STAMP(ta);
+            asm volatile("" ::"v"(cand[0].v[0]), "v"(cand[1].v[0]), "v"(cand[2].v[0]), "v"(cand[0].v[2]), "v"(cand[1].v[2]),
+                         "v"(cand[2].v[2]));
+            P2PMG_STAMP(tb);
+            trA0 += ta - tr1;
+            trWC += tb - ta;
+            trMid = tb;
+          }
 #endif
+          ip = (int)((ipc0 >> (8 * b)) & 0xFFu);
+          rowR = patched(sel_row(b, cand[0], cand[1], cand[2]), strip + (uint32_t)ip, pat);
+        } else {
+          float acc = 0.0f;
+#pragma unroll
+          for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : col[j]));
+          ip = p2p_bin(fdiv_b(div_n_r<N>(acc, rn), rmi));
+          const bool need = code == 255 || (TRAIN && r == R1 - 1);
+#if P2PMG_ABLATE == 7
+          rowR = fake_row(q + (need ? strip + (uint32_t)ip : a0) * kQPad);
+#else
+          rowR = gat((need ? strip + (uint32_t)ip : a0));
+#endif
+        }
+#if P2PMG_BAT_SPEC
+        // the final round's battery rule for each of the 3 actions while its row is in flight (it
+        // needs only balw, the level and this step's SoC): the action then only selects
+        float outA[3];
+        double socA[3];
+        if constexpr (BAT != 0) {
+          if (r == R1 - 1) {
+#pragma unroll
+            for (int x = 0; x < 3; ++x) {
+              socA[x] = soc;
+              outA[x] = balw + hp_of(lv, x);
+              if (bcap > 0.0) outA[x] = bat_rule(outA[x], socA[x]);
+            }
+          }
+        }
+#endif
+        act = code == 255 ? argmax3(rowR) : code;
+        acts |= (uint32_t)act << (8 * r);
+        ips |= (uint32_t)ip << (8 * r);
+        hp = hp_of(lv, act);
+        if (r == R1 - 1) {
+#if P2PMG_TRACE
+          {
+            uint64_t tc;
+            asm volatile("" ::"v"(act));
+            P2PMG_STAMP(tc);
+            trA1 += tc - trMid;
+            trMid = tc;
+          }
+#endif
+          issue_next(act);
+#if P2PMG_TRACE
+          P2PMG_STAMP(trLast);
+          trC += trLast - trMid;
+#endif
+          refill_words();
+          settle_next();
+        }
+        float out = balw + hp;
+        if constexpr (BAT != 0) {
+#if P2PMG_BAT_SPEC
+          if (r == R1 - 1) {
+            const Sel3M m = sel3_masks(act);
+            out = sel3(m, outA[0], outA[1], outA[2]);
+            soc_r = sel3(m, socA[0], socA[1], socA[2]);
+          } else
+#endif
+          {
+            soc_r = soc;
+            if (bcap > 0.0) out = bat_rule(out, soc_r);
+          }
+        }
+#if P2PMG_ABLATE == 11  // timing-only: no final-round divide-power and no market (cost from out alone)
+        if (r == R1 - 1) {
+          row[0] = out;
+          continue;
+        }
+#endif
+        // _divide_power's filter keeps pw where sign(out) != sign(pw) (agent.py:187-188): for out > 0
+        // that is pw <= 0, for out < 0 pw >= 0, for out = 0 any pw.  A kept pw = +-0 and a dropped
+        // one (0) are interchangeable: every later use is |f| or a sum that already holds +0.
+        // As one clamp: f = med3(pw, out < 0 ? 0 : -inf, out > 0 ? 0 : +inf).
+        const float flo = out < 0.0f ? 0.0f : -__builtin_inff(), fhi = out > 0.0f ? 0.0f : __builtin_inff();
+        float f[N];
+        float tot = 0.0f;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          const float pw = -((j == i) ? 0.0f : col[j]);
+          f[j] = __builtin_amdgcn_fmed3f(pw, flo, fhi);
+          tot = tot + f[j];
+        }
+        tot = fabsf(tot);
+        const float ev = div_n_r<N>(out * 1.0f, rn);
+        // out * |f_j| / tot for every j: the diagonal's f_ii = +-0 gives out * 0 / tot = out * 0, the
+        // reference's value for it (agent.py:193-194), for any tot > 0.  One range guard per round.
+        const Recip rt = recip(tot == 0.0f ? 1.0f : tot);  // the tot = 0 lanes take ev
+        const float nout = nabs_out(out);
+        float num[N];
+        bool bad = !rt.ok;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          num[j] = nout * f[j];
+          row[j] = fdiv_core(num[j], rt);
+          bad = bad || !fdiv_ok(num[j]);
+        }
+        if (bad) {
+#pragma unroll
+          for (int j = 0; j < N; ++j) row[j] = fdiv_ieee(num[j], rt.b);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) row[j] = (tot == 0.0f) ? ev : row[j];
+      }
+      soc = soc_r;  // BatteryStorage state after the final round's decision
+      pat.row = 0xFFFFFFFFu;  // the next step's rows were issued after the previous TD store
+
+      // CommunityMicrogrid._assign_powers community.py:45-54 on the final P (diagonal kept)
+      float g = 0.0f, pp = 0.0f;
+#if P2PMG_ABLATE == 11
+      g = row[0];
+#else
+      exchange<N>(row, col, i, sl, nullptr);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        // ex = sign(pij) * min(|pij|, |pji|) where the signs differ (community.py:48-50)
+        const float pij = row[j], pji = col[j];
+        const float ex = pair_exchange(pij, pji);
+        g = g + (pij - ex);
+        pp = pp + ex;
+      }
+#endif
+      // CommunityMicrogrid._compute_costs community.py:56-65
+      float cost = (g >= 0.0f) ? g * e0.buy : g * e0.inj;
+      cost = cost + pp * e0.p2p;
+      cost = fdiv_b(cost * k.slot, rmph);
+      cost = cost * k.kilo;
+      // RLAgent.get_reward agent.py:225-232 (pre-update T_in)
+      float pen = fmaxf(fmaxf(0.0f, k.lower - tin), fmaxf(0.0f, tin - k.upper));
+      pen = pen > 0.0f ? pen + 1.0f : 0.0f;
+      const float rw = -(cost + k.penw * pen);
+
+      if constexpr (TRAIN) {
+        // QAgent.train agent.py:293-298 -> QActor.train rl.py:119-129
+        const uint32_t srow = strip + (uint32_t)ip;
+        const QT qsa = sel3(act, rowR.v[0], rowR.v[1], rowR.v[2]);
+        const QT qnew = td_update(qsa, rw, max3(patched(rowN, aN, pprev)), k.alpha, k.gamma);
+        *(active ? q + srow * kQPad + act : q_dummy) = qnew;
+#if P2PMG_ABLATE == 9 || P2PMG_ABLATE == 10
+        pat = Patch<QT>{0xFFFFFFFFu, 0, (QT)0};  // timing-only: the next step does not wait for this TD
+#else
+        pat = Patch<QT>{srow, act, qnew};  // rows issued before this store see the old value
+#endif
+      }
+      if constexpr (narrow) {
+        *reinterpret_cast<float2*>(__builtin_assume_aligned(rec_ptr, 8)) = make_float2(rw, cost);
+      } else {
+        const uint32_t bins = (p0.y & 0xFFFFu) | ((uint32_t)iT << 16);  // it * nT*nb + ib | iT << 16
+        float4* rp = reinterpret_cast<float4*>(__builtin_assume_aligned(rec_ptr, 16));
+        rp[0] = make_float4(rw, cost, g, pp);
+        rp[1] = make_float4(tin, __uint_as_float(acts), __uint_as_float(bins), __uint_as_float(ips));
+      }
+      rec_ptr += rec_step;
+      // step t's env row and pre-pass word are dead: step t + 3's into their slots (the barrier keeps
+      // the scheduler from hoisting the loads above the old values' last use, which would need a
+      // second register set and a copy at the loop's back edge)
+      asm volatile("" ::: "memory");
+      eS[P] = load_envv(envb + eo3);
+      pS[P] = preb[o3];
+      // avg_reward = sum_t mean_i r (community.py:179), canonical sequential order
+      const float m = group_sum<N>(rw, lane, i, sl, nullptr);
+      ep_sum = ep_sum + div_n_r<N>(m, rn);
+
+      tin = tin1;
+      tm = tm1;
+      iT = iT1;
+      o3 += (uint32_t)A;
+      o3 = o3 == TA ? 0u : o3;
+      eo3 += env_st;
+      eo3 = eo3 == env_end ? 0u : eo3;
+      strip = strip1;
+      cw = cw1;
+      a0 = a0n;
+      aN = aNn;
+      row0 = row0n;
+      rowN = rowNn;
+      if constexpr (CAND) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) cand[b] = candn[b];
+      }
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    using S2 = std::integral_constant<int, 2>;
+    int t = 0;
+    for (; t + 3 <= T; t += 3) {
+      step(S0{});
+      step(S1{});
+      step(S2{});
+    }
+    if (t < T) step(S0{});
+    if (t + 1 < T) step(S1{});
+#if P2PMG_TRACE
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || (int)blockIdx.x == n_cons / 2 || (int)blockIdx.x == n_cons - 1))
+      printf("TRACE blk %d/%d T %d: per step wait %.1f round0 %.1f waitcand %.1f round1 %.1f issue %.1f rest %.1f "
+             "(one stamp %.1f)\n",
+             (int)blockIdx.x, n_cons, T, (double)trW / T, (double)trA0 / T, (double)trWC / T, (double)trA1 / T,
+             (double)trC / T, (double)trR / (T - 1), (double)trCal / T);
+#endif
+    if (active) {
+      if (p.reset_t0) {  // agent.reset() at the end of train_episode (community.py:181), fused
+        tin = t0_in;
+        tm = t0_m;
+      }
+      if (i == 0) {
+        if (p.chain_rewards) p.chain_rewards[(size_t)ep * p.S + s] = ep_sum;
+        if (ep == n_chain - 1) p.ep_reward[s] = ep_sum;
+      }
+    }
+  }  // chain
   if (active) {
-    if (p.reset_t0)  // agent.reset() at the end of train_episode (community.py:181), fused
-      t0_draw(p.seed_lo, p.seed_hi, p.episode + 1, p.agent_offset + (uint32_t)a, p.setpoint, p.reset_sigma, tin, tm);
     p.t_in[a] = tin;
     p.t_m[a] = tm;
     if constexpr (BAT != 0) p.soc[a] = soc;
-    if (i == 0) p.ep_reward[s] = ep_sum;
   }
 }
 
@@ -2513,7 +2539,7 @@ hipError_t launch_battery_seq(int agents, int steps, const double* bal, double* 
 hipError_t launch_step_prepass(const EpisodeParams& p, const PrepOut& o, hipStream_t stream) {
   const size_t n = (size_t)p.T * p.A;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(step_prepass_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, p, o);
+  hipLaunchKernelGGL(step_prepass_kernel, dim3(grid_for(n, 256), o.n_ep > 1 ? o.n_ep : 1), dim3(256), 0, stream, p, o);
   return hipGetLastError();
 }
 #endif

@@ -59,11 +59,14 @@ struct p2pmg_ctx {
   // never Q or T); run_episode(e + 1) uses it when its arguments match (spec_*), else recomputes.
   uint2* pre[2] = {nullptr, nullptr};        // [T][A] {balw, bins}
   uint32_t* pre_ipc[2] = {nullptr, nullptr}; // N = 2: [T][A] round-1 bins per partner action
-  uint32_t* pcodes[2] = {nullptr, nullptr};  // Philox code words [T][W][A]
+  uint32_t* pcodes[2] = {nullptr, nullptr};  // Philox code words [T][W][A], one per episode of a chain
+  size_t pcodes_cap[2] = {0, 0};             // ... their capacity in words
   int pslot = 0;
   bool spec_valid[2] = {false, false};
   int spec_episode[2] = {0, 0};
-  double spec_eps[2] = {0.0, 0.0};
+  std::vector<double> spec_chain[2];         // the epsilons of the chain a slot holds (one: {eps})
+  float* chain_rew = nullptr;                // p2pmg_run_episodes: [n][S] episode rewards of the last call
+  int chain_rew_cap = 0, chain_n = 0;
   long long spec_version[2] = {-1, -1};
   long long inputs_version = 0;  // bumped by every input upload (env, profiles, max_in, hp levels)
   long long spec_hits = 0, spec_misses = 0;  // fast-path launches whose pre-pass was / was not ready
@@ -353,10 +356,12 @@ int p2pmg_destroy(p2pmg_ctx* c) {
     dfree(c->pre[k]);
     dfree(c->pre_ipc[k]);
     dfree(c->pcodes[k]);
+    c->pcodes_cap[k] = 0;
   }
   if (c->dummy) (void)hipFree(c->dummy);
   if (c->rec_pack) (void)hipFree(c->rec_pack);
   dfree(c->ep_reward);
+  dfree(c->chain_rew);
   dfree(c->d_metrics);
   dfree(c->d_hash);
   for (auto& b : c->rec_f32) dfree(b);
@@ -658,7 +663,35 @@ static bool host_div_range(float b) {
   return m >= 0x1p-40f && m <= 0x1p40f;
 }
 
-int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
+// fast per-agent-table path (episode_fast_kernel): automatic whenever it applies
+static bool fast_applies(const p2pmg_ctx* c, const p2pmg_episode_args* args) {
+  static const bool env_general = [] { const char* v = getenv("P2PMG_KERNEL"); return v && !strcmp(v, "general"); }();
+  const p2pmg_config& g = c->cfg;
+  return !g.shared_q && (!c->battery || c->R + 1 <= p2pmg::kFastBatMaxR1) && c->N <= 8 && c->R + 1 <= 4 && c->mi_ok &&
+         (long long)g.n_time_states * g.n_temp_states * g.n_balance_states < 65536 &&
+         // a wave's 64 tables span < 4 GiB (the gathers' 32-bit offsets)
+         64LL * g.n_time_states * g.n_temp_states * g.n_balance_states * g.n_p2p_states * 4 * (g.q_dtype == 0 ? 8 : 4) <
+             (1LL << 32) &&
+         (long long)c->T * c->A < (1LL << 32) && host_div_range(g.minutes_per_hour) &&
+         g.temp_margin == 1.0f &&  // heating.py:90 (the kernel skips the / margin)
+         !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_PHILOX_INKERNEL)) && !env_general;
+}
+
+// a chained fast-path launch (p2pmg_run_episodes): n episodes at eps[0..n), the caller's guess of
+// the next chain (next_n episodes at next_eps) for the speculative pre-pass, rewards [n][S] on device
+struct ChainReq {
+  int n;
+  const double* eps;
+  int next_n;
+  const double* next_eps;
+  float* rewards;
+};
+
+static int run_episode_impl(p2pmg_ctx* c, const p2pmg_episode_args* args, const ChainReq* ch);
+
+int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) { return run_episode_impl(c, args, nullptr); }
+
+static int run_episode_impl(p2pmg_ctx* c, const p2pmg_episode_args* args, const ChainReq* ch) {
   if (!c || !args) return P2PMG_E_INVALID;
   if (c->dqn) return dqn_run_episode(c, args);
   if (!c->have_env || !c->have_prof || !c->have_params)
@@ -670,18 +703,11 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     return fail(c, P2PMG_E_STATE, "run_episode: replay mode needs p2pmg_set_replay_codes");
   int rc = P2PMG_OK;
   const p2pmg_config& g = c->cfg;
-  // fast per-agent-table path (episode_fast_kernel): automatic whenever it applies
   static const int env_spw = [] { const char* v = getenv("P2PMG_SPW"); return v ? atoi(v) : 0; }();
   static const bool env_general = [] { const char* v = getenv("P2PMG_KERNEL"); return v && !strcmp(v, "general"); }();
-  const bool fast = !g.shared_q && (!c->battery || c->R + 1 <= p2pmg::kFastBatMaxR1) && c->N <= 8 &&
-                    c->R + 1 <= 4 && c->mi_ok &&
-                    (long long)g.n_time_states * g.n_temp_states * g.n_balance_states < 65536 &&
-                    // a wave's 64 tables span < 4 GiB (the gathers' 32-bit offsets)
-                    64LL * g.n_time_states * g.n_temp_states * g.n_balance_states * g.n_p2p_states * 4 *
-                            (g.q_dtype == 0 ? 8 : 4) < (1LL << 32) &&
-                    (long long)c->T * c->A < (1LL << 32) && host_div_range(g.minutes_per_hour) &&
-                    g.temp_margin == 1.0f &&  // heating.py:90 (the kernel skips the / margin)
-                    !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_PHILOX_INKERNEL)) && !env_general;
+  const bool fast = fast_applies(c, args);
+  if (ch && !(fast && train && args->rng == P2PMG_RNG_PHILOX))
+    return fail(c, P2PMG_E_INVALID, "run_episode: a chained launch needs the fast kernel and Philox training");
   // shared table, 16-agent scenarios (configs[2]): episode_sq16_kernel
   const bool sq16 = g.shared_q && c->N == 16 && c->R <= 1 && c->mi_ok && host_div_range(g.minutes_per_hour) &&
                     (long long)c->T * c->A < (1LL << 32) && (long long)c->T * c->n_env * p2pmg::kEnvStride < (1LL << 32) &&
@@ -701,44 +727,72 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   bool produce = false;
   if (fast) {
     const size_t ta = (size_t)c->T * c->A;
+    const size_t wpe = ta * ((c->R + 4) / 4);  // code words per episode
     const bool philox = train && args->rng == P2PMG_RNG_PHILOX;
     const bool want_ipc = c->N == 2 && c->R >= 1 && !c->battery;  // the kernel's CAND path
+    // this launch's chain (one episode unless chained) and the caller's guess of the next launch's:
+    // P2PMG_FLAG_NEXT_EPSILON: next_epsilon is the guess as given (0 included); without it a
+    // positive next_epsilon is the guess and anything else means "the same epsilon"
+    std::vector<double> cur(ch ? ch->eps : &args->epsilon, ch ? ch->eps + ch->n : &args->epsilon + 1);
+    std::vector<double> nxt_eps;
+    if (ch) {
+      if (ch->next_n > 0) nxt_eps.assign(ch->next_eps, ch->next_eps + ch->next_n);
+      else nxt_eps.assign(cur.size(), cur.back());
+    } else {
+      const bool have_next = (args->flags & P2PMG_FLAG_NEXT_EPSILON) != 0 || args->next_epsilon > 0.0;
+      nxt_eps.assign(1, have_next ? args->next_epsilon : args->epsilon);
+    }
+    const int n_ep = (int)cur.size(), n_next = (int)nxt_eps.size();
     for (int k = 0; k < 2; ++k) {  // both slots (the launch writes the other one)
       if (!c->pre[k]) HIP_TRY(c, dmalloc(&c->pre[k], ta));
       if (want_ipc && !c->pre_ipc[k]) HIP_TRY(c, dmalloc(&c->pre_ipc[k], ta));
-      if (philox && !c->pcodes[k]) HIP_TRY(c, dmalloc(&c->pcodes[k], ta * ((c->R + 4) / 4)));
+      const size_t need = wpe * (size_t)std::max(n_ep, n_next);
+      if (philox && c->pcodes_cap[k] < need) {
+        dfree(c->pcodes[k]);
+        c->pcodes_cap[k] = 0;
+        c->spec_valid[k] = false;
+        HIP_TRY(c, dmalloc(&c->pcodes[k], need));
+        c->pcodes_cap[k] = need;
+      }
     }
     p.pre_ipc = want_ipc ? c->pre_ipc[ps] : nullptr;
     if (philox) p.codes = c->pcodes[ps];
     p.rng = 0;
+    p.chain = n_ep;
+    p.codes_stride = wpe;
+    p.chain_rewards = ch ? ch->rewards : nullptr;
     if (args->record && !c->rec_pack) HIP_TRY(c, hipMalloc(&c->rec_pack, ta * p2pmg::kFastRecBytes));
+    auto prep_out = [&](int slot, int episode, const std::vector<double>& eps) {
+      p2pmg::PrepOut o{c->pre[slot], want_ipc ? c->pre_ipc[slot] : nullptr, philox ? c->pcodes[slot] : nullptr,
+                       episode, eps[0], 0u, 0};
+      p2pmg::eps_threshold(eps[0], o.eps_thr, o.eps_all);
+      o.n_ep = (int)eps.size();
+      o.words_stride = wpe;
+      o.ep_all = 0;
+      for (int k = 0; k < o.n_ep; ++k) {
+        int all = 0;
+        p2pmg::eps_threshold(eps[k], o.ep_thr[k], all);
+        o.ep_all |= (uint64_t)all << k;
+      }
+      return o;
+    };
     // this slot's pre-pass: computed by the previous launch if it guessed these arguments
     const bool hit = c->spec_valid[ps] && c->spec_version[ps] == c->inputs_version &&
-                     (!philox || (c->spec_episode[ps] == args->episode && c->spec_eps[ps] == args->epsilon));
-    if (!hit) {
-      const p2pmg::PrepOut o{c->pre[ps], p.pre_ipc, philox ? c->pcodes[ps] : nullptr, args->episode,
-                             args->epsilon, p.eps_thr, p.eps_all};
-      HIP_TRY(c, p2pmg::launch_step_prepass(p, o, c->stream));
-    }
-    // the next slot, for episode + 1 at the caller's next epsilon (the decay schedule is known,
-    // community.py:279-286; <= 0: the same epsilon).  Philox draws only when this one has them.
+                     (!philox || (c->spec_episode[ps] == args->episode && c->spec_chain[ps] == cur));
+    if (!hit) HIP_TRY(c, p2pmg::launch_step_prepass(p, prep_out(ps, args->episode, cur), c->stream));
+    // the next slot, for the episodes after this launch's at the caller's guess (the decay schedule
+    // is known, community.py:279-286).  Philox draws only when this one has them.
     // P2PMG_NO_SPEC=1 (profiling only): no producer blocks, so the episode kernel's counters are its own
     static const bool env_no_spec = [] { const char* v = getenv("P2PMG_NO_SPEC"); return v && atoi(v) != 0; }();
     const int ns = ps ^ 1;
-    // P2PMG_FLAG_NEXT_EPSILON: next_epsilon is the guess as given (0 included); without it a
-    // positive next_epsilon is the guess and anything else means "the same epsilon"
-    const bool have_next = (args->flags & P2PMG_FLAG_NEXT_EPSILON) != 0 || args->next_epsilon > 0.0;
-    const double next_eps = have_next ? args->next_epsilon : args->epsilon;
-    next = p2pmg::PrepOut{c->pre[ns], want_ipc ? c->pre_ipc[ns] : nullptr, philox ? c->pcodes[ns] : nullptr,
-                          args->episode + 1, next_eps, 0u, 0};
-    p2pmg::eps_threshold(next_eps, next.eps_thr, next.eps_all);
+    next = prep_out(ns, args->episode + n_ep, nxt_eps);
     produce = !env_no_spec;
     if (hit) c->spec_hits++;
     else c->spec_misses++;
     c->spec_valid[ns] = produce;
     c->spec_version[ns] = c->inputs_version;
-    c->spec_episode[ns] = philox ? args->episode + 1 : -1;
-    c->spec_eps[ns] = next_eps;
+    c->spec_episode[ns] = philox ? args->episode + n_ep : -1;
+    c->spec_chain[ns] = nxt_eps;
   } else if (train && args->rng == P2PMG_RNG_PHILOX) {
     bool prepass = c->A < (1 << 18) && !sq16;  // sq16: throughput-bound, draws in the kernel
     if (args->flags & P2PMG_FLAG_PHILOX_PREPASS) prepass = true;
@@ -809,6 +863,66 @@ int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   }
   c->timed = true;
   if (stamp) c->n_timed++;
+  return P2PMG_OK;
+}
+
+int p2pmg_run_episodes(p2pmg_ctx* c, const p2pmg_episode_args* args, int n, const double* epsilons, int next_n,
+                       const double* next_epsilons) {
+  if (!c || !args || n < 1 || !epsilons || (next_n > 0 && !next_epsilons)) return P2PMG_E_INVALID;
+  if (!c->dqn && (!c->have_env || !c->have_prof || !c->have_params))
+    return fail(c, P2PMG_E_STATE, "run_episodes: env, profiles and agent params must be set first");
+  if (c->chain_rew_cap < n) {  // at least one full chain's worth, so a caller's chains never reallocate
+    const int cap = std::max(n, p2pmg::kMaxChain);
+    dfree(c->chain_rew);
+    c->chain_rew_cap = 0;
+    HIP_TRY(c, dmalloc(&c->chain_rew, (size_t)cap * c->S));
+    c->chain_rew_cap = cap;
+  }
+  c->chain_n = 0;
+  const bool chain = !c->dqn && args->mode == P2PMG_MODE_TRAIN && args->rng == P2PMG_RNG_PHILOX && fast_applies(c, args);
+  p2pmg_episode_args a = *args;
+  if (!chain) {  // one launch per episode, the same results
+    for (int k = 0; k < n; ++k) {
+      a.episode = args->episode + k;
+      a.epsilon = epsilons[k];
+      a.flags = args->flags | P2PMG_FLAG_NEXT_EPSILON;
+      a.next_epsilon = k + 1 < n ? epsilons[k + 1] : next_n > 0 ? next_epsilons[0] : epsilons[k];
+      const int rc = p2pmg_run_episode(c, &a);
+      if (rc != P2PMG_OK) return rc;
+      HIP_TRY(c, hipMemcpyAsync(c->chain_rew + (size_t)k * c->S, c->ep_reward,
+                                (size_t)c->S * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+    }
+    c->chain_n = n;
+    return P2PMG_OK;
+  }
+  // chains of at most kMaxChain episodes whose code words fit 1 GiB per slot
+  const size_t wpe_bytes = (size_t)c->T * c->A * ((c->R + 4) / 4) * sizeof(uint32_t);
+  const int per = (int)std::max<size_t>(1, std::min<size_t>(p2pmg::kMaxChain, ((size_t)1 << 30) / wpe_bytes));
+  for (int k0 = 0; k0 < n; k0 += per) {
+    const int m = std::min(per, n - k0);
+    const int k1 = k0 + m;
+    ChainReq req{m, epsilons + k0, 0, nullptr, c->chain_rew + (size_t)k0 * c->S};
+    if (k1 < n) {
+      req.next_n = std::min(per, n - k1);
+      req.next_eps = epsilons + k1;
+    } else if (next_n > 0) {
+      req.next_n = std::min(per, next_n);
+      req.next_eps = next_epsilons;
+    }
+    a.episode = args->episode + k0;
+    a.epsilon = epsilons[k0];
+    const int rc = run_episode_impl(c, &a, &req);
+    if (rc != P2PMG_OK) return rc;
+  }
+  c->chain_n = n;
+  return P2PMG_OK;
+}
+
+int p2pmg_get_episode_rewards(p2pmg_ctx* c, int n, float* host) {
+  if (!c || !host || n < 0) return P2PMG_E_INVALID;
+  if (n > c->chain_n) return fail(c, P2PMG_E_STATE, "get_episode_rewards: the last run_episodes call ran fewer episodes");
+  HIP_TRY(c, hipMemcpyAsync(host, c->chain_rew, (size_t)n * c->S * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return P2PMG_OK;
 }
 

@@ -260,6 +260,36 @@ class DeviceCommunityBatch:
         self._chk(self.L.p2pmg_run_episode(self._ctx, C.byref(args)), "run_episode")
         self._recorded = mask
 
+    def run_episodes(self, episode: int, epsilons, reset_sigma: Optional[float] = None,
+                     next_epsilons=None, scen_per_wave: int = 0, record: Sequence[str] = ()):
+        """Train len(epsilons) consecutive episodes with Philox draws (community.py:279-286's loop
+        body): episode + k at epsilons[k], each ending with the T0 reset when reset_sigma is given.
+        Where the fast kernel applies, chained launches run up to 64 episodes each, every wave
+        going through its episodes back to back; results are those of run_episode per episode,
+        bit for bit.  next_epsilons: the next call's epsilons (its speculative pre-pass).  record:
+        what the last episode leaves in the record buffers (as after run_episode per episode)."""
+        eps = np.ascontiguousarray(np.asarray(epsilons, dtype=np.float64).reshape(-1))
+        flags = _lib.FLAG_RESET_T0 if reset_sigma is not None else 0
+        mask = 0
+        for r in record:
+            mask |= _lib.REC[r]
+        args = _lib.EpisodeArgs(_lib.MODE_TRAIN, _lib.RNG_PHILOX, int(episode), mask, float(eps[0]), flags,
+                                int(scen_per_wave), float(reset_sigma or 0.0), 0.0)
+        nxt = None if next_epsilons is None else np.ascontiguousarray(np.asarray(next_epsilons, np.float64).reshape(-1))
+        self._chain_eps = (eps, nxt)  # kept alive for the call
+        self._chk(self.L.p2pmg_run_episodes(self._ctx, C.byref(args), int(eps.size), eps,
+                                            0 if nxt is None else int(nxt.size),
+                                            None if nxt is None else nxt.ctypes.data), "run_episodes")
+        self._recorded = mask
+        self._chain_len = int(eps.size)
+
+    def episode_rewards(self) -> np.ndarray:
+        """[n, S] episode rewards (community.py:179) of every episode of the last run_episodes."""
+        n = getattr(self, "_chain_len", 0)
+        out = np.empty((n, self.S), F32)
+        self._chk(self.L.p2pmg_get_episode_rewards(self._ctx, n, out), "get_episode_rewards")
+        return out
+
     def run_rule_episode(self, record: Sequence[str] = ()):
         """CommunityMicrogrid.run of a RuleAgent community (community.py:95-123, 237-238; agent.py:106-136):
         hysteresis heat pumps, no policy, R = 0.  Records: cost, grid, p2p, t_in, action (0 off, 2 on)."""
