@@ -752,13 +752,19 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
     # next metric point back to back in every wave; same results as one launch per episode
     chain = not shared and args.chain == "auto"
     launch_eps = []  # episodes of every launch since the last reset_kernel_times (chained mode)
+    launch_log = []  # [first episode, episodes] of every chained launch of this context (rocprof trace split)
+    # the schedule as one array, sliced per chain (building the lists inside the timed region cost ~30 us)
+    sched = np.array([epsilon_at(e) for e in range(max(schedule_to, warmup + steps) + 2 * MAX_CHAIN
+                                                   + args.metric_every)])
 
     def first_chain(e0, e1):  # the episodes of the first launch of episodes(e0, e1)
         return min(e1, e0 + args.metric_every, e0 + MAX_CHAIN) - e0
 
     def episodes(e0, e1, metric=True, next_end=None):
         """Episodes [e0, e1) with the metric all-reduce every --metric-every episodes and after the
-        last; next_end: where the caller's next episodes(e1, next_end) ends (the pre-pass guess)."""
+        last; next_end: where the caller's next episodes(e1, next_end) ends (the pre-pass guess).
+        The call's last chain guesses at most its own length of the next call's episodes (its
+        producers run inside it), except untimed (metric=False) calls, which guess exactly."""
         if not chain:
             for k, e in enumerate(range(e0, e1)):
                 episode(e)
@@ -768,10 +774,14 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
         k0 = e0
         while k0 < e1:
             k1 = k0 + first_chain(k0, e1)
-            n_next = first_chain(k1, e1) if k1 < e1 else (first_chain(e1, next_end) if next_end else k1 - k0)
-            eng.run_episodes(k0, [epsilon_at(e) for e in range(k0, k1)], reset_sigma=0.3, record=record,
-                             next_epsilons=[epsilon_at(e) for e in range(k1, k1 + n_next)])
+            if k1 < e1:
+                n_next = first_chain(k1, e1)
+            else:
+                n_next = first_chain(e1, next_end) if next_end else k1 - k0
+                n_next = n_next if not metric else min(n_next, k1 - k0)
+            eng.run_episodes(k0, sched[k0:k1], reset_sigma=0.3, record=record, next_epsilons=sched[k1:k1 + n_next])
             launch_eps.append(k1 - k0)
+            launch_log.append([k0, k1 - k0])
             if metric:
                 metrics[0] = episode_metrics(eng, world, comm_err)  # every chain ends at a metric point
             k0 = k1
@@ -893,6 +903,8 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
                          "timed_launches": int(len(kms)), "timing_period": timing_period},
             "mean_episode_reward": ep_reward,
             "epsilon_range": [epsilon_at(warmup), epsilon_at(warmup + steps - 1)],
+            "launch": ({"mode": "chained (p2pmg_run_episodes)", "launches": launch_log} if chain
+                       else {"mode": "one launch per episode"}),
             "rccl_nranks": nranks,
             "rank_times_s": rank_times,
         }

@@ -685,6 +685,7 @@ struct ChainReq {
   int next_n;
   const double* next_eps;
   float* rewards;
+  int reserve;  // code-word capacity to allocate, in episodes (every chain of the call fits)
 };
 
 static int run_episode_impl(p2pmg_ctx* c, const p2pmg_episode_args* args, const ChainReq* ch);
@@ -747,12 +748,13 @@ static int run_episode_impl(p2pmg_ctx* c, const p2pmg_episode_args* args, const 
       if (!c->pre[k]) HIP_TRY(c, dmalloc(&c->pre[k], ta));
       if (want_ipc && !c->pre_ipc[k]) HIP_TRY(c, dmalloc(&c->pre_ipc[k], ta));
       const size_t need = wpe * (size_t)std::max(n_ep, n_next);
-      if (philox && c->pcodes_cap[k] < need) {
+      if (philox && c->pcodes_cap[k] < need) {  // chains: their full capacity at once (no reallocation later)
+        const size_t cap = std::max(need, wpe * (size_t)(ch ? ch->reserve : 1));
         dfree(c->pcodes[k]);
         c->pcodes_cap[k] = 0;
         c->spec_valid[k] = false;
-        HIP_TRY(c, dmalloc(&c->pcodes[k], need));
-        c->pcodes_cap[k] = need;
+        HIP_TRY(c, dmalloc(&c->pcodes[k], cap));
+        c->pcodes_cap[k] = cap;
       }
     }
     p.pre_ipc = want_ipc ? c->pre_ipc[ps] : nullptr;
@@ -901,7 +903,7 @@ int p2pmg_run_episodes(p2pmg_ctx* c, const p2pmg_episode_args* args, int n, cons
   for (int k0 = 0; k0 < n; k0 += per) {
     const int m = std::min(per, n - k0);
     const int k1 = k0 + m;
-    ChainReq req{m, epsilons + k0, 0, nullptr, c->chain_rew + (size_t)k0 * c->S};
+    ChainReq req{m, epsilons + k0, 0, nullptr, c->chain_rew + (size_t)k0 * c->S, per};
     if (k1 < n) {
       req.next_n = std::min(per, n - k1);
       req.next_eps = epsilons + k1;

@@ -268,14 +268,14 @@ class DeviceCommunityBatch:
         going through its episodes back to back; results are those of run_episode per episode,
         bit for bit.  next_epsilons: the next call's epsilons (its speculative pre-pass).  record:
         what the last episode leaves in the record buffers (as after run_episode per episode)."""
-        eps = np.ascontiguousarray(np.asarray(epsilons, dtype=np.float64).reshape(-1))
+        eps = np.ascontiguousarray(epsilons, dtype=np.float64).reshape(-1)
         flags = _lib.FLAG_RESET_T0 if reset_sigma is not None else 0
         mask = 0
         for r in record:
             mask |= _lib.REC[r]
         args = _lib.EpisodeArgs(_lib.MODE_TRAIN, _lib.RNG_PHILOX, int(episode), mask, float(eps[0]), flags,
                                 int(scen_per_wave), float(reset_sigma or 0.0), 0.0)
-        nxt = None if next_epsilons is None else np.ascontiguousarray(np.asarray(next_epsilons, np.float64).reshape(-1))
+        nxt = None if next_epsilons is None else np.ascontiguousarray(next_epsilons, dtype=np.float64).reshape(-1)
         self._chain_eps = (eps, nxt)  # kept alive for the call
         self._chk(self.L.p2pmg_run_episodes(self._ctx, C.byref(args), int(eps.size), eps,
                                             0 if nxt is None else int(nxt.size),

@@ -6,7 +6,9 @@ the configs[1] warm-up (episodes 0-4), the timed region (5-24) and the epsilon-s
 continuation (25-999, value_at_eps), then episode_sq16_kernel for the configs[2] secondary
 (2 warm-up + 10 timed).  rocprofv3 --stats averages over every launch, so its configs[1] average
 is mostly the continuation (lower epsilon, slower episodes); this script splits the trace by launch
-index so each phase's average can be set beside the HIP-event kernel_ms of the bench line.
+index so each phase's average can be set beside the HIP-event kernel_ms of the bench line.  With
+chained launches (the line's launch.launches: [first episode, episodes] per launch) each launch's
+duration is split evenly over its episodes; the phase averages are per episode.
 
     python scripts/summarize_trace.py gpurun_out/r05/prof_c2/c2_kernel_trace.csv gpurun_out/r05/c2.json \
         > profiles/r05_bench_kernel_phases.json
@@ -26,12 +28,28 @@ def avg(xs):
     return sum(xs) / len(xs) if xs else None
 
 
+def per_episode(fast, line):
+    """Per-episode kernel time in episode order: chained launches (line["launch"]["launches"] =
+    [first episode, episodes] in launch order) split evenly over their episodes."""
+    launches = (line.get("launch") or {}).get("launches")
+    if not launches:
+        return fast
+    assert len(launches) == len(fast), (len(launches), len(fast))
+    out = []
+    for (first, n), d in zip(launches, fast):
+        assert first == len(out), (first, len(out))
+        out += [d / n] * n
+    return out
+
+
 def main(trace, line_path):
     line = json.loads(open(line_path).read().strip().splitlines()[-1])
     w, k = line["warmup"], line["steps"]
-    fast = durations(trace, "episode_fast_kernel")
+    launch_us = durations(trace, "episode_fast_kernel")
+    fast = per_episode(launch_us, line)
     out = {"trace": trace, "line": line_path, "episode_fast_kernel": {
-        "launches": len(fast), "all_launches_us": avg(fast),
+        "launches": len(launch_us), "episodes": len(fast), "all_launches_us": avg(launch_us),
+        "all_episodes_us": avg(fast),
         "timed_region": {"episodes": [w, w + k], "avg_us": avg(fast[w:w + k]),
                          "line_kernel_ms": line["roofline"]["kernel_ms"]}}}
     ve = line.get("value_at_eps")
