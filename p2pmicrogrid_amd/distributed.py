@@ -248,5 +248,22 @@ class ShardedTrainer:
         self.episode += 1
         return float(total / count)
 
+    def train_episodes(self, epsilons, reset_sigma: float = 0.3, next_epsilons=None) -> np.ndarray:
+        """len(epsilons) training episodes on every shard (community.py:279-286's loop body, each
+        ending with agent.reset()); returns the global mean episode reward of each.  Per-agent
+        tables run as chained launches (p2pmg_run_episodes: the episodes back to back in every
+        wave, results identical to train_episode per episode); a shared table or DQN network needs
+        its exchange between episodes and runs train_episode per episode."""
+        eps = [float(e) for e in epsilons]
+        if self.learner == "dqn" or self.shared_q:
+            out = [self.train_episode(e, reset_sigma, eps[k + 1] if k + 1 < len(eps) else None)
+                   for k, e in enumerate(eps)]
+            return np.array(out)
+        self.eng.run_episodes(self.episode, eps, reset_sigma=reset_sigma, next_epsilons=next_epsilons)
+        local = self.eng.episode_rewards().astype(np.float64)  # [n, S]
+        tot = all_reduce_sum(np.concatenate([local.sum(axis=1), [local.shape[1]]]), self.world)
+        self.episode += len(eps)
+        return tot[:-1] / tot[-1]
+
     def episode_rewards_global(self) -> np.ndarray:
         return all_gather_concat(self.eng.episode_reward(), self.world)

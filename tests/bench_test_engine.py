@@ -27,17 +27,6 @@ class BenchOracleEngine(OracleEngine):
             self.reset_temperatures_philox(episode + 1, reset_sigma)
         self._times.append(float("nan"))
 
-    def run_episodes(self, episode, epsilons, reset_sigma=None, next_epsilons=None, record=()):
-        """p2pmg_run_episodes: the same episodes one by one (the device chains them in one launch)."""
-        self._chain = []
-        for k, eps in enumerate(epsilons):
-            self.run_episode("train", "philox", episode=episode + k, epsilon=eps, record=record,
-                             reset_sigma=reset_sigma)
-            self._chain.append(self.episode_reward())
-
-    def episode_rewards(self):
-        return np.stack(self._chain)
-
     def comm_init(self, uid, rank, world):
         raise RuntimeError("no RCCL in the CPU test engine")
 

@@ -50,6 +50,18 @@ class OracleEngine:
     def episode_reward(self):
         return self.last["episode_reward"]
 
+    def run_episodes(self, episode, epsilons, reset_sigma=None, next_epsilons=None, record=()):
+        """p2pmg_run_episodes: the same episodes one by one (the device chains them in one launch)."""
+        self._chain = []
+        for k, eps in enumerate(epsilons):
+            self.run_episode("train", "philox", episode=episode + k, epsilon=eps, record=record)
+            if reset_sigma is not None:
+                self.reset_temperatures_philox(episode + k + 1, reset_sigma)
+            self._chain.append(self.episode_reward())
+
+    def episode_rewards(self):
+        return np.stack(self._chain)
+
     def set_battery(self, capacity, min_soc=0.1, max_soc=0.9, efficiency=0.9, soc0=0.5):
         ob = self._ensure()
         ob.battery_capacity = np.broadcast_to(np.asarray(capacity, np.float64), (self.S, self.N)).copy()

@@ -26,8 +26,12 @@ def _worker(rank, world, port, q, kw):
     from oracle_engine import OracleEngine
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    chain = kw.pop("_chain", False)
     tr = ShardedTrainer(S_TOTAL, N, R, T, rank=rank, world=world, engine_factory=OracleEngine, **kw)
-    means = [tr.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    if chain:  # train_episodes: chained launches on the device, one per call
+        means = list(tr.train_episodes([0.81 * 0.9 ** e for e in range(EPISODES)]))
+    else:
+        means = [tr.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
     per_scen = tr.episode_rewards_global()
     if rank == 0:
         q.put((means, per_scen, tr.eng.get_q(0, 1) if kw.get("shared_q") else None))
@@ -66,6 +70,19 @@ def test_two_rank_gloo_matches_single_process():
     means1 = [single.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
     per1 = single.episode_rewards_global()
     means2, per2, _ = _run_two_ranks({})
+    assert np.array_equal(per1, per2)
+    assert np.allclose(means1, means2, rtol=0, atol=1e-9)
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_train_episodes_match_single_process_episode_loop():
+    """ShardedTrainer.train_episodes (chained launches per rank) over gloo at world 2 equals the
+    single-process train_episode loop: per-scenario rewards and the global means."""
+    from oracle_engine import OracleEngine
+    single = ShardedTrainer(S_TOTAL, N, R, T, engine_factory=OracleEngine)
+    means1 = [single.train_episode(0.81 * 0.9 ** e) for e in range(EPISODES)]
+    per1 = single.episode_rewards_global()
+    means2, per2, _ = _run_two_ranks({"_chain": True})
     assert np.array_equal(per1, per2)
     assert np.allclose(means1, means2, rtol=0, atol=1e-9)
 

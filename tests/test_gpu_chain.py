@@ -129,3 +129,17 @@ def test_chain_leaves_the_last_episodes_records(record):
     for k in record:
         assert np.array_equal(ra[k], rb[k]), k
     _same_state(a, b)
+
+
+def test_sharded_trainer_train_episodes_equals_episode_loop():
+    """ShardedTrainer.train_episodes (chained launches) against its train_episode loop (one launch and
+    a separate T0 reset per episode): the same global means, tables and temperatures."""
+    from p2pmicrogrid_amd.distributed import ShardedTrainer
+    a = ShardedTrainer(40, 2, 1, 24)
+    b = ShardedTrainer(40, 2, 1, 24)
+    eps = _schedule(0, 6)
+    m1 = [a.train_episode(e) for e in eps]
+    m2 = b.train_episodes(eps)
+    assert np.array_equal(np.array(m1), m2)
+    _same_state(a.eng, b.eng)
+    assert a.episode == b.episode == 6
