@@ -66,6 +66,10 @@ struct p2pmg_ctx {
   int spec_episode[2] = {0, 0};
   std::vector<double> spec_chain[2];         // the epsilons of the chain a slot holds (one: {eps})
   float* chain_rew = nullptr;                // p2pmg_run_episodes: [n][S] episode rewards of the last call
+  // pinned host staging of the small per-episode read-backs (episode rewards, metrics): a pageable
+  // destination takes HIP's staged copy path (~26 us for 16 KB with the device idle)
+  void* h_small = nullptr;
+  size_t h_small_bytes = 0;
   int chain_rew_cap = 0, chain_n = 0;
   long long spec_version[2] = {-1, -1};
   long long inputs_version = 0;  // bumped by every input upload (env, profiles, max_in, hp levels)
@@ -381,6 +385,7 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   dfree(c->d_grad);
   dfree(c->d_segs);
   if (c->h_segs) (void)hipHostFree(c->h_segs);
+  if (c->h_small) (void)hipHostFree(c->h_small);
   dfree(c->d_smp);
   dfree(c->d_buf);
   dfree(c->d_added);
@@ -1079,11 +1084,24 @@ int p2pmg_prepass_stats(p2pmg_ctx* c, int64_t* hits, int64_t* misses) {
   return P2PMG_OK;
 }
 
+// device -> caller's host memory through the pinned staging buffer (stream-ordered, then synced)
+static int read_small(p2pmg_ctx* c, void* host, const void* dev, size_t bytes) {
+  if (c->h_small_bytes < bytes) {
+    if (c->h_small) (void)hipHostFree(c->h_small);
+    c->h_small = nullptr;
+    c->h_small_bytes = 0;
+    HIP_TRY(c, hipHostMalloc(&c->h_small, bytes, hipHostMallocDefault));
+    c->h_small_bytes = bytes;
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->h_small, dev, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  std::memcpy(host, c->h_small, bytes);
+  return P2PMG_OK;
+}
+
 int p2pmg_get_episode_reward(p2pmg_ctx* c, float* host) {
   if (!c || !host) return P2PMG_E_INVALID;
-  HIP_TRY(c, hipMemcpyAsync(host, c->ep_reward, (size_t)c->S * 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  return P2PMG_OK;
+  return read_small(c, host, c->ep_reward, (size_t)c->S * 4);
 }
 
 int p2pmg_rc_step(p2pmg_ctx* c, int n, const float* t_out, const float* t_in, const float* t_m, const float* hp,
@@ -1372,9 +1390,7 @@ int p2pmg_allreduce_metrics(p2pmg_ctx* c, double* out) {
     const int rc = r->allReduce(c->d_metrics, c->d_metrics, 2, 8, 0, c->comm, c->stream);
     if (rc != 0) return fail(c, P2PMG_E_HIP, std::string("ncclAllReduce(metrics): ") + (r->getErrorString ? r->getErrorString(rc) : "?"));
   }
-  HIP_TRY(c, hipMemcpyAsync(out, c->d_metrics, 16, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  return P2PMG_OK;
+  return read_small(c, out, c->d_metrics, 16);
 }
 
 int p2pmg_table_hash_allgather(p2pmg_ctx* c, uint64_t* out) {
