@@ -844,6 +844,11 @@ static int run_episode_impl(p2pmg_ctx* c, const p2pmg_episode_args* args, const 
     const int full = 64 / (c->N <= 1 ? 1 : c->N <= 2 ? 2 : c->N <= 4 ? 4 : 8);
     const int waves = (c->S + full - 1) / full;
     spw = waves >= c->n_cu ? full : std::max(full / 4, (c->S + c->n_cu - 1) / c->n_cu);
+    // below epsilon 0.5 most lanes are greedy (a round-0 row gather and two argmaxes on every step):
+    // there half-filled waves, two per CU, measured faster (configs[1], chained: 80.7 -> 77.9 us per
+    // episode at epsilon 0.1, 76.1 -> 75.0 at 0.39, even at 0.53), above it one wave per CU
+    // (71.7 against 73.9 us at 0.729): profiles/r05_chain/spw_epsilon.txt
+    if (fast && train && args->epsilon < 0.5 && waves < c->n_cu) spw = std::max(full / 4, (spw + 1) / 2);
     spw = std::min(spw, full);
   }
   const bool reset = (args->flags & P2PMG_FLAG_RESET_T0) != 0;

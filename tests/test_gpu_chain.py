@@ -143,3 +143,24 @@ def test_sharded_trainer_train_episodes_equals_episode_loop():
     assert np.array_equal(np.array(m1), m2)
     _same_state(a.eng, b.eng)
     assert a.episode == b.episode == 6
+
+
+def test_low_epsilon_wave_split_keeps_results():
+    """configs[1]'s batch (4096 scenarios: one wave per CU) below epsilon 0.5 runs half-filled waves
+    (two per CU): the same tables, temperatures and rewards as one full wave per CU."""
+    S, N, R, T = 4096, 2, 1, 12
+    inp = scenario_batch(S, N, T, seed=59)
+    eng = _device_for(inp, N, R)
+    out = []
+    for spw in (0, 16):
+        eng.zero_q()
+        eng.set_temperatures(inp.t_in0, inp.t_m0)
+        eng.run_episodes(0, [0.3, 0.3, 0.3], reset_sigma=0.3, scen_per_wave=spw)
+        out.append((eng.episode_rewards(), eng.get_temperatures(), eng.get_q(first=0, count=64),
+                    eng.get_q(first=S * N - 64, count=64)))
+    for x, y in zip(out[0], out[1]):
+        if isinstance(x, tuple):
+            for u, v in zip(x, y):
+                assert np.array_equal(u, v)
+        else:
+            assert np.array_equal(x, y)
