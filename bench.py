@@ -734,8 +734,8 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
     metrics = [None]
 
     def episode(e):
-        if shared:
-            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record,
+        if shared:  # agent.reset() at the end of train_episode fused into the launch, as below
+            eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record, reset_sigma=0.3,
                             next_epsilon=epsilon_at(e + 1))
             if world > 1 and xk == "host":
                 from p2pmicrogrid_amd.distributed import all_reduce_int64
@@ -743,8 +743,7 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
             elif world > 1 or (args.rccl_world1 and not comm_err):
                 eng.allreduce_q_delta()
             eng.apply_q_delta()
-            eng.reset_temperatures_philox(e + 1, 0.3)  # agent.reset() at the end of train_episode
-        else:  # the same reset, fused into the episode launch
+        else:
             eng.run_episode("train", "philox", episode=e, epsilon=epsilon_at(e), record=record, reset_sigma=0.3,
                             next_epsilon=epsilon_at(e + 1))
 
