@@ -892,7 +892,8 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
                                        else f"scenario-sharded x{world} (replicas, no data-path collective)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
+                         # per episode where the PMC summary has it (chained launches), else per launch
+                         "traffic": (traffic or {}).get("hbm_bytes_per_episode", (traffic or {}).get("hbm_bytes_per_launch")),
                          "kernel": eng.last_kernel(),
                          "kernel_ms": kernel_ms,  # per episode (a chained launch runs several)
                          "kernel_ms_per_launch": float(np.mean(kms)) if len(kms) else None,
