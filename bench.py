@@ -675,6 +675,17 @@ def load_traffic(path: str, workload: str):
 
 
 MAX_CHAIN = 64  # episodes per chained launch (p2pmg.h p2pmg_run_episodes)
+def traffic_per_episode(traffic, chained: bool):
+    """HBM bytes per episode from a PMC summary (profiles/pmc_traffic*.json): its chained-launch
+    figure when the run chained its episodes, its one-launch-per-episode figure otherwise."""
+    if not traffic:
+        return None
+    if chained and "hbm_bytes_per_episode" in traffic:
+        return traffic["hbm_bytes_per_episode"]
+    single = traffic.get("one_launch_per_episode")
+    return (single or traffic).get("hbm_bytes_per_launch")
+
+
 REFERENCE_EPISODES = 1000  # setup.py:30 max_episodes: the reference's training run (community.py:272-298)
 
 
@@ -892,8 +903,8 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
                                        else f"scenario-sharded x{world} (replicas, no data-path collective)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         # per episode where the PMC summary has it (chained launches), else per launch
-                         "traffic": (traffic or {}).get("hbm_bytes_per_episode", (traffic or {}).get("hbm_bytes_per_launch")),
+                         # per episode: the PMC summary's chained figure, or its one-launch-per-episode one
+                         "traffic": traffic_per_episode(traffic, chain),
                          "kernel": eng.last_kernel(),
                          "kernel_ms": kernel_ms,  # per episode (a chained launch runs several)
                          "kernel_ms_per_launch": float(np.mean(kms)) if len(kms) else None,
