@@ -1,6 +1,7 @@
 """CPU tests of the host side: the C-ABI library loads and exports every symbol declared in
 include/p2pmg.h (no compute calls needing a GPU), the native replay decoder reproduces the
 reference's np.random consumption, datasets follow the reference schema, bench helpers."""
+import json
 import os
 import re
 
@@ -128,6 +129,15 @@ def test_bench_helpers():
     g = bench.gather_roofline(8192, 96, 0.080)
     assert g is not None and 0.0 < g["floor"] < 80.0 and abs(g["frac"] - g["floor"] / 80.0) < 1e-12
     assert bench.gather_roofline(4096, 96, 0.080) is None and bench.gather_roofline(8192, 672, 0.080) is None
+    # the issue roofline only at the counter pass's sizes (configs[2]: 125,000 x 16, R = 1, T = 96)
+    assert bench.issue_roofline("config3", 2.7, (125000, 16, 1, 96)) is not None
+    assert bench.issue_roofline("config3", 2.7, (15625, 16, 1, 96)) is None
+    # PMC traffic per episode: the chained figure for chained runs, the one-launch-per-episode one otherwise
+    t = bench.load_traffic(os.path.join(bench.ROOT, "profiles", "pmc_traffic.json"),
+                           json.load(open(os.path.join(bench.ROOT, "profiles", "pmc_traffic.json")))["workload"])
+    assert bench.traffic_per_episode(t, True) == t["hbm_bytes_per_episode"]
+    assert bench.traffic_per_episode(t, False) == t["one_launch_per_episode"]["hbm_bytes_per_launch"]
+    assert bench.traffic_per_episode(None, True) is None
 
 
 def test_device_count_without_gpu_is_zero_or_more():
