@@ -164,3 +164,24 @@ def test_low_epsilon_wave_split_keeps_results():
                 assert np.array_equal(u, v)
         else:
             assert np.array_equal(x, y)
+
+
+def test_full_size_chain_equals_single_launches():
+    """configs[1] at full size (4096 scenarios, T = 96) over the bench's schedule: a 50-episode chain
+    (epsilon 0.729) and a 20-episode chain below epsilon 0.5 (half-filled waves) equal the same
+    episodes launched one by one: every episode's rewards, temperatures, and the whole tables'
+    fingerprints."""
+    import bench
+    S, N, R, T = 4096, 2, 1, 96
+    inp = scenario_batch(S, N, T)
+    a, b = _device_for(inp, N, R), _device_for(inp, N, R)
+    for e0, n in ((1, 50), (251, 20)):
+        eps = [bench.epsilon_at(e) for e in range(e0, e0 + n)]
+        rew = _singles(a, e0, eps)
+        b.run_episodes(e0, eps, reset_sigma=0.3)
+        assert np.array_equal(b.episode_rewards(), rew), e0
+        for x, y in zip(a.get_temperatures(), b.get_temperatures()):
+            assert np.array_equal(x, y)
+    assert np.array_equal(a.table_hash_allgather(), b.table_hash_allgather())
+    a.close()
+    b.close()
