@@ -695,7 +695,10 @@ struct ChainReq {
 
 static int run_episode_impl(p2pmg_ctx* c, const p2pmg_episode_args* args, const ChainReq* ch);
 
-int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) { return run_episode_impl(c, args, nullptr); }
+int p2pmg_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
+  if (c) c->chain_n = 0;  // p2pmg_get_episode_rewards covers p2pmg_run_episodes calls only
+  return run_episode_impl(c, args, nullptr);
+}
 
 static int run_episode_impl(p2pmg_ctx* c, const p2pmg_episode_args* args, const ChainReq* ch) {
   if (!c || !args) return P2PMG_E_INVALID;
@@ -899,7 +902,7 @@ int p2pmg_run_episodes(p2pmg_ctx* c, const p2pmg_episode_args* args, int n, cons
       a.epsilon = epsilons[k];
       a.flags = args->flags | P2PMG_FLAG_NEXT_EPSILON;
       a.next_epsilon = k + 1 < n ? epsilons[k + 1] : next_n > 0 ? next_epsilons[0] : epsilons[k];
-      const int rc = p2pmg_run_episode(c, &a);
+      const int rc = run_episode_impl(c, &a, nullptr);
       if (rc != P2PMG_OK) return rc;
       HIP_TRY(c, hipMemcpyAsync(c->chain_rew + (size_t)k * c->S, c->ep_reward,
                                 (size_t)c->S * sizeof(float), hipMemcpyDeviceToDevice, c->stream));

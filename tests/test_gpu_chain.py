@@ -90,7 +90,9 @@ def test_long_chain_splits_and_speculates_the_next_call():
 
 
 def test_chain_without_reset_and_after_single_launches():
-    """No T0 reset (temperatures carry over between episodes), interleaved with single launches."""
+    """No T0 reset (temperatures carry over between episodes), interleaved with single launches;
+    the per-episode rewards of a chain are only readable until the next single launch."""
+    from p2pmicrogrid_amd._lib import P2PMGError
     S, N, R, T = 24, 2, 1, 20
     inp = scenario_batch(S, N, T, seed=43)
     a, b = _device_for(inp, N, R), _device_for(inp, N, R)
@@ -101,6 +103,12 @@ def test_chain_without_reset_and_after_single_launches():
         a.run_episode("train", "philox", episode=e, epsilon=0.4)
     b.run_episodes(2, [0.4] * 4)
     _same_state(a, b)
+    assert b.episode_rewards().shape == (4, S)
+    a.run_episode("train", "philox", episode=6, epsilon=0.4)
+    b.run_episode("train", "philox", episode=6, epsilon=0.4)
+    _same_state(a, b)
+    with pytest.raises(P2PMGError):
+        b.episode_rewards()
 
 
 def test_fallback_where_the_fast_kernel_does_not_apply():
