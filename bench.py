@@ -820,6 +820,7 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
     dt, rank_times = timed(eng, world, lambda: episodes(warmup, warmup + steps, next_end=nxt_end))
     kms = eng.kernel_times()
     kernel_ms_ep = kernel_ms_per_episode(kms)
+    timed_launch_eps = list(launch_eps)  # the timed region's launches (the schedule's reuse the list)
     coll = collective_record(eng, world, steps, world1=args.rccl_world1 and not comm_err)
     ep_reward = metrics[0][0] / metrics[0][1]
     nranks = eng.comm_nranks() if not comm_err else 0
@@ -908,11 +909,11 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
                          "kernel": eng.last_kernel(),
                          "kernel_ms": kernel_ms,  # per episode (a chained launch runs several)
                          "kernel_ms_per_launch": float(np.mean(kms)) if len(kms) else None,
-                         "episodes_per_launch": list(launch_eps) if chain else 1,
+                         "episodes_per_launch": timed_launch_eps if chain else 1,
                          "algorithmic_bytes_per_agent_step": bpa,
                          "algorithmic_bytes_per_episode": bpa * steps_per_episode,
                          "algorithmic_bytes_per_launch": bpa * steps_per_episode * (
-                             float(np.mean(launch_eps)) if chain and launch_eps else 1.0),
+                             float(np.mean(timed_launch_eps)) if chain and timed_launch_eps else 1.0),
                          "timed_launches": int(len(kms)), "timing_period": timing_period},
             "mean_episode_reward": ep_reward,
             "epsilon_range": [epsilon_at(warmup), epsilon_at(warmup + steps - 1)],
