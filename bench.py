@@ -459,8 +459,9 @@ def main_dqn(args, rank, world, local, S, N, R, T):
         if (k + 1) % args.metric_every == 0 or k + 1 == args.steps:
             metrics = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
     eng.sync()
+    t1 = time.perf_counter()  # before the trailing barrier, as in timed()
     barrier(world)
-    rank_times = all_gather_float(time.perf_counter() - t0, world)
+    rank_times = all_gather_float(t1 - t0, world)
     dt = max(rank_times)
     kms = eng.kernel_times()
     coll = collective_record(eng, world, args.steps, "RCCL allGather of the gradient segments (data path)",
@@ -690,15 +691,19 @@ REFERENCE_EPISODES = 1000  # setup.py:30 max_episodes: the reference's training 
 
 
 def timed(eng, world, fn):
-    """Run fn() between a barrier + device sync on both sides; the MAX of every rank's wall time."""
+    """Run fn() between a barrier + device sync on both sides; the MAX of every rank's wall time.
+    A rank's clock runs from the leading barrier's release to its own device sync after fn(): the
+    trailing barrier still brackets the region (no rank moves on early) but its own latency (a gloo
+    round over the host, ~0.1 ms at 8 ranks against a 1.5 ms configs[1] region) is not work."""
     eng.sync()
     barrier(world)
     eng.sync()
     t0 = time.perf_counter()
     fn()
     eng.sync()
+    t1 = time.perf_counter()
     barrier(world)
-    rank_times = all_gather_float(time.perf_counter() - t0, world)
+    rank_times = all_gather_float(t1 - t0, world)
     return max(rank_times), rank_times
 
 
