@@ -371,6 +371,16 @@ def test_bench_default_line_carries_configs2_secondary_and_value_at_eps(world, d
     assert s["config"]["shared_q"] and s["config"]["battery"] and s["config"]["agent_steps_per_step"] == 8 * 4 * 12
     assert s["steps"] == 2 and s["value"] > 0 and s["ms_per_step"] > 0 and "roofline" in s
     assert s["table_replicas_identical"]
+    # per-agent tables run chained launches: contiguous from episode 0 to the schedule's end, at most
+    # 64 episodes each, every one ending at a metric point of its call (warm-up 1, timed 2, the
+    # schedule's calls to the windows at 6 and 15 and to episode 24); the timed call is one launch
+    la = d["launch"]
+    assert la["mode"].startswith("chained")
+    firsts = [f for f, _ in la["launches"]]
+    assert firsts[0] == 0 and all(f + n == g for (f, n), g in zip(la["launches"], firsts[1:]))
+    assert sum(n for _, n in la["launches"]) == 24 and all(1 <= n <= 64 for _, n in la["launches"])
+    assert [1, 2] == [n for f, n in la["launches"] if f in (0, 1)]
+    assert {6, 9, 15, 18} <= set(firsts) and d["roofline"]["episodes_per_launch"] == [2]
     if world > 1:
         assert len(d["launcher"]["rank_exit_codes"]) == world
         assert s["exchange"] == "host-rehearsal" and "exchange_fallback" in s  # no RCCL in the test engine
