@@ -75,7 +75,7 @@ template <typename T>
 __device__ __forceinline__ T sel3(int a, T x0, T x1, T x2) {
   return sel3(sel3_masks(a), x0, x1, x2);
 }
-// Timing-only ablation builds (scripts/latency_ablation.py): -DP2PMG_ABLATE=1 replaces the
+// Timing-only ablation builds (scripts/dev/latency_ablation.py): -DP2PMG_ABLATE=1 replaces the
 // episode kernel's Q-row gathers by values derived from the address (no memory access),
 // -DP2PMG_ABLATE=2 replaces f32 divisions by reciprocal multiplies; in the fast kernel =8 fakes the
 // next step's rows, =9 cuts the TD -> next-step patch dependency, =10 both, =11 drops the final
