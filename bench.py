@@ -410,12 +410,14 @@ def cpu_baseline_dqn(seconds: float, S: int = 2, N: int = 2, R: int = 1, T: int 
                       f"episodes after one fill episode, oracle/dqn.py NumPy, {dt:.1f} s"}
 
 
-def main_dqn(args, rank, world, local, S, N, R, T):
+def run_dqn(args, rank, world, local, S, N, R, T, steps, warmup, cpu_seconds):
     """configs[4]: DQN agents with ONE shared Q-network (data-parallel): every env step runs the
     act launch (greedy forwards on the Q-MLP, market, reward, replay append, RC update) and the
-    train launch (32-sample batches on f32 MFMA) + gradient reduce (+ RCCL all-reduce over ranks)
-    + Adam/soft update.  One bench step = one training episode (T env steps) of every scenario."""
+    train launch (32-sample batches on f32 MFMA) + gradient reduce (+ RCCL all-gather of the
+    gradient segments over ranks) + Adam/soft update.  One bench step = one training episode
+    (T env steps) of every scenario.  Rank 0 returns the record, the other ranks None."""
     from p2pmicrogrid_amd.dataset import scenario_batch
+    t_setup = time.perf_counter()
     first = rank * S
     inp = scenario_batch(S, N, T, first_scenario=first)
     dkw = {}
@@ -430,12 +432,15 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     eng.set_temperatures(inp.t_in0, inp.t_m0)
     del inp
     xk = exchange_kind(args, world)
+    fallback, comm_err = None, ""
+    if xk != "host":  # gradient-segment all-gather every env step + metrics over RCCL
+        comm_err = rccl_comm(eng, rank, world, required=args.exchange == "rccl", world1=args.rccl_world1)
+        if comm_err and world > 1:  # --exchange auto without a communicator: the labelled host exchange
+            fallback, xk = comm_err, "host"
     if xk == "host":  # rehearsal: the gradient segments gathered over gloo every env step
         from p2pmicrogrid_amd.distributed import all_gather_rows
         eng.set_grad_exchange(lambda rows: all_gather_rows(rows, rank, world), rank, world)
-        comm_err = "host-rehearsal exchange (no RCCL communicator)"
-    else:  # gradient-segment all-gather every env step + metrics over RCCL
-        comm_err = rccl_comm(eng, rank, world, required=True, world1=args.rccl_world1)
+        comm_err = comm_err or "host-rehearsal exchange (no RCCL communicator)"
     record = ("reward", "cost")
     eng.run_episode("fill", "philox", episode=0, epsilon=1.0, record=record)  # community.init_buffers
     eng.reset_temperatures_philox(1, 0.3)
@@ -444,9 +449,11 @@ def main_dqn(args, rank, world, local, S, N, R, T):
         eng.run_episode("train", "philox", episode=e, epsilon=0.9 ** e, record=record)
         eng.reset_temperatures_philox(e + 1, 0.3)
 
-    for e in range(1, 1 + args.warmup):
+    eng.sync()
+    t_fill = time.perf_counter() - t_setup
+    for e in range(1, 1 + warmup):
         episode(e)
-    if world > 1 and args.warmup > 0:  # the first metric all-reduce sets up the communicator: not timed
+    if world > 1 and warmup > 0:  # the first metric all-reduce sets up the communicator: not timed
         episode_metrics(eng, world, comm_err)
     eng.sync()
     eng.reset_kernel_times()
@@ -454,9 +461,9 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     eng.sync()
     t0 = time.perf_counter()
     metrics = None
-    for k, e in enumerate(range(1 + args.warmup, 1 + args.warmup + args.steps)):
+    for k, e in enumerate(range(1 + warmup, 1 + warmup + steps)):
         episode(e)
-        if (k + 1) % args.metric_every == 0 or k + 1 == args.steps:
+        if (k + 1) % args.metric_every == 0 or k + 1 == steps:
             metrics = episode_metrics(eng, world, comm_err)  # RCCL, the reference's 50-episode log
     eng.sync()
     t1 = time.perf_counter()  # before the trailing barrier, as in timed()
@@ -464,7 +471,7 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     rank_times = all_gather_float(t1 - t0, world)
     dt = max(rank_times)
     kms = eng.kernel_times()
-    coll = collective_record(eng, world, args.steps, "RCCL allGather of the gradient segments (data path)",
+    coll = collective_record(eng, world, steps, "RCCL allGather of the gradient segments (data path)",
                              world1=args.rccl_world1 and not comm_err)
     # every rank's replica of the shared network (the same Adam step on the same gathered sum)
     from p2pmicrogrid_amd.distributed import all_gather_concat
@@ -473,10 +480,11 @@ def main_dqn(args, rank, world, local, S, N, R, T):
     flop = dqn_flop_per_agent_step(R)
     episode_ms = float(np.mean(kms)) if len(kms) else float("nan")
     achieved = flop * steps_per_episode / (episode_ms * 1e-3) / 1e12
+    out = None
     if rank == 0:
         out = {
-            "metric": METRIC, "value": world * steps_per_episode * args.steps / dt, "unit": "agent-steps/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "metric": METRIC, "value": world * steps_per_episode * steps / dt, "unit": "agent-steps/s",
+            "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": dt / steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic profiles with the reference dataset schema (seed 42), Glorot-uniform init",
             "config": {"workload": f"configs[4]: {S} scenarios/GPU x {N} DQN agents (R={R}, T={T}), one shared "
@@ -495,22 +503,24 @@ def main_dqn(args, rank, world, local, S, N, R, T):
             "rank_times_s": rank_times,
             "grad_layout": eng.grad_layout(),
             "network_replicas_identical": bool(np.all(fps == fps[0])),
+            "setup_s": {"inputs_context_and_fill_episode": t_fill},
         }
         assert out["network_replicas_identical"], f"shared-network replicas differ across ranks: {fps}"
         if world > 1:
             out["exchange"] = "host-rehearsal" if xk == "host" else "rccl"
+        if fallback:
+            out["exchange_fallback"] = f"RCCL unavailable ({fallback}): gradient segments gathered over gloo"
         if coll and xk != "host":
             out["collective"] = coll
-        if world == 1 and not args.no_cpu_baseline:
-            workers, rule = cpu_workers()
-            out["cpu_baseline"] = cpu_baseline_all_cores("cpu_baseline_dqn", dict(seconds=args.cpu_seconds, R=R, T=T),
-                                                         workers)
-            out["cpu_baseline"].update(os_cpu_count=os.cpu_count(), cores_rule=rule)
-        print(json.dumps(out), flush=True)
+        if os.environ.get("P2PMG_BENCH_TEST_DQN_ENGINE"):
+            out["test_engine"] = os.environ["P2PMG_BENCH_TEST_DQN_ENGINE"]
     eng.close()
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_seconds > 0:
+        workers, rule = cpu_workers()
+        out["cpu_baseline"] = cpu_baseline_all_cores("cpu_baseline_dqn", dict(seconds=cpu_seconds, R=R, T=T),
+                                                     workers)
+        out["cpu_baseline"].update(os_cpu_count=os.cpu_count(), cores_rule=rule)
+    return out
 
 
 def cpu_baseline(seconds: float, S: int = 256, N: int = 2, R: int = 1, T: int = 96, q_dtype: str = "f64",
@@ -676,6 +686,7 @@ def load_traffic(path: str, workload: str):
 
 
 MAX_CHAIN = 64  # episodes per chained launch (p2pmg.h p2pmg_run_episodes)
+PARALLEL_GEN_ELEMS = 100_000_000  # agent-slots above which the inputs are generated by a worker pool
 def traffic_per_episode(traffic, chained: bool):
     """HBM bytes per episode from a PMC summary (profiles/pmc_traffic*.json): its chained-launch
     figure when the run chained its episodes, its one-launch-per-episode figure otherwise."""
@@ -714,24 +725,33 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
     return None.  schedule_to > 0 (per-agent tables): the same context then continues the
     reference's epsilon schedule up to that episode (community.py:272-298), timing `window_steps`
     episodes from each start in eps_windows and the whole continuation (value_at_eps)."""
-    from p2pmicrogrid_amd.dataset import apply_asset_mix, asset_mix, scenario_batch
+    from p2pmicrogrid_amd.dataset import SharedScenarioInputs, apply_asset_mix, asset_mix, scenario_batch
+    t_setup = time.perf_counter()
     DeviceCommunityBatch = engine_class()
     S0, N0, R0, T0, qd0, shared, battery = WORKLOADS[wl]
     hetero = wl in HETERO
     S, N, T, q_dtype = S or S0, N or N0, T or T0, q_dtype or qd0
     R = R0 if R is None else R
     first = rank * S
-    inp = scenario_batch(S, N, T, first_scenario=first)
-    mix = None
-    if hetero:
-        mix = asset_mix(S, N, first_scenario=first, battery_j=BATTERY_J)
-        inp = apply_asset_mix(inp, mix)
+    mix = asset_mix(S, N, first_scenario=first, battery_j=BATTERY_J) if hetero else None
+    gen = None
+    if S * N * T >= PARALLEL_GEN_ELEMS and not os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
+        # configs[3]'s year of profiles (9.2 GB per GPU): generator blocks on the host cores, into shared memory
+        gen = SharedScenarioInputs(S, N, T, cpu_workers()[0], first_scenario=first, mix=mix)
+        inp = gen.inputs
+    else:
+        inp = scenario_batch(S, N, T, first_scenario=first)
+        if hetero:
+            inp = apply_asset_mix(inp, mix)
+    t_gen = time.perf_counter() - t_setup
     eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=local, scenario_offset=first, shared_q=shared)
     eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
     eng.set_profiles(inp.load_w, inp.pv_w)
     eng.set_max_in(inp.max_in)
     eng.set_temperatures(inp.t_in0, inp.t_m0)
     del inp
+    if gen is not None:
+        gen.close()
     if mix is not None:
         eng.set_hp_levels(mix.hp_levels)
         eng.set_battery(mix.battery_capacity)
@@ -811,6 +831,8 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
             return float(np.mean(kms))
         return float(np.sum(kms)) / float(np.sum(launch_eps[-len(kms):]))
 
+    eng.sync()
+    t_upload = time.perf_counter() - t_setup - t_gen
     episodes(0, warmup, metric=False, next_end=warmup + steps)
     if world > 1 and warmup > 0:  # the first collective on a communicator sets up its connections: not timed
         episode_metrics(eng, world, comm_err)
@@ -926,6 +948,10 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
                        else {"mode": "one launch per episode"}),
             "rccl_nranks": nranks,
             "rank_times_s": rank_times,
+            # outside the timed region: host input generation (parallel above PARALLEL_GEN_ELEMS) and the
+            # context build + upload + zeroed tables
+            "setup_s": {"inputs": t_gen, "context_and_upload": t_upload,
+                        "input_generation": "parallel (dataset.SharedScenarioInputs)" if gen is not None else "serial"},
         }
         if os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
             out["test_engine"] = os.environ["P2PMG_BENCH_TEST_ENGINE"]
@@ -1033,6 +1059,14 @@ def main():
     ap.add_argument("--secondary-steps", type=int, default=10)
     ap.add_argument("--secondary-warmup", type=int, default=2)
     ap.add_argument("--secondary-cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--extra", default="auto",
+                    help="further workloads measured by the same ranks after the secondary, comma-separated (auto: "
+                         "config5,config4 = configs[4] DQN and configs[3] one-year mixes after the default config2; "
+                         "'' = none)")
+    ap.add_argument("--extra-scenarios", type=int, default=None, help="override the extras' scenarios per GPU")
+    ap.add_argument("--extra-horizon", type=int, default=None, help="override the extras' horizon")
+    ap.add_argument("--extra-steps", type=int, default=5)
+    ap.add_argument("--extra-warmup", type=int, default=1)
     args = ap.parse_args()
     if args.gpus is not None and args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
@@ -1046,7 +1080,13 @@ def main():
     if args.workload == "config5":
         S, N, R, T, _, _, _ = WORKLOADS["config5"]
         R = R if args.rounds is None else args.rounds
-        main_dqn(args, rank, world, local, args.scenarios or S, args.agents or N, R, args.horizon or T)
+        out = run_dqn(args, rank, world, local, args.scenarios or S, args.agents or N, R, args.horizon or T,
+                      args.steps, args.warmup, args.cpu_seconds)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
         return 0
     sched = args.schedule_episodes
     if sched is None:
@@ -1074,6 +1114,31 @@ def main():
             for k in ("metric", "higher_is_better", "scaling", "vs_baseline", "n_gpus"):
                 sec.pop(k, None)
             out["secondary"] = sec
+    # the other BASELINE configs on the same ranks, after the primary line's (auto: behind the default
+    # configs[1] + configs[2]): configs[4] (DQN, the gradient-segment all-gather over xGMI at world > 1)
+    # and configs[3] (one-year heterogeneous episodes)
+    extra = args.extra
+    if extra == "auto":
+        extra = "config5,config4" if args.workload == "config2" else ""
+    for wl in [x.strip() for x in extra.split(",") if x.strip() and x.strip() != args.workload]:
+        key = {"config5": "secondary_dqn", "config4": "secondary_year"}.get(wl, f"secondary_{wl}")
+        try:
+            if wl == "config5":
+                S5, N5, R5, T5, _, _, _ = WORKLOADS["config5"]
+                rec = run_dqn(args, rank, world, local, args.extra_scenarios or S5, N5, R5, args.extra_horizon or T5,
+                              args.extra_steps, args.extra_warmup, args.secondary_cpu_seconds)
+            else:
+                rec = run_tabular(args, rank, world, local, wl, S=args.extra_scenarios, T=args.extra_horizon,
+                                  steps=args.extra_steps, warmup=args.extra_warmup,
+                                  cpu_seconds=args.secondary_cpu_seconds)
+        except Exception as e:  # noqa: BLE001  (the primary line stands; the failure is reported in it)
+            print(f"bench.py: extra workload {wl} failed on rank {rank}: {type(e).__name__}: {e}",
+                  file=sys.stderr, flush=True)
+            rec = {"error": f"{type(e).__name__}: {e}", "workload": wl}
+        if rank == 0:
+            for k in ("metric", "higher_is_better", "scaling", "vs_baseline", "n_gpus"):
+                rec.pop(k, None)
+            out[key] = rec
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

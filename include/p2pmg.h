@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define P2PMG_ABI_VERSION 7  /* 3: p2pmg_episode_args.next_epsilon; 4: P2PMG_FLAG_NEXT_EPSILON, p2pmg_prepass_stats, per-network Adam steps; 5: p2pmg_collective_ms; 6: DQN gradient segments, p2pmg_dqn_set_exchange, p2pmg_dqn_grad_layout; 7: p2pmg_run_episodes, p2pmg_get_episode_rewards */
+#define P2PMG_ABI_VERSION 8  /* 3: p2pmg_episode_args.next_epsilon; 4: P2PMG_FLAG_NEXT_EPSILON, p2pmg_prepass_stats, per-network Adam steps; 5: p2pmg_collective_ms; 6: DQN gradient segments, p2pmg_dqn_set_exchange, p2pmg_dqn_grad_layout; 7: p2pmg_run_episodes, p2pmg_get_episode_rewards; 8: N up to 64 and any R, P2PMG_FLAG_TILE_KERNEL */
 
 typedef struct p2pmg_ctx p2pmg_ctx;
 
@@ -47,7 +47,7 @@ typedef struct p2pmg_ctx p2pmg_ctx;
 #define P2PMG_E_HIP 2         /* HIP runtime error (message in p2pmg_last_error) */
 #define P2PMG_E_NOMEM 3       /* device allocation failed */
 #define P2PMG_E_STATE 4       /* missing prerequisite (e.g. profiles not set) */
-#define P2PMG_E_UNSUPPORTED 5 /* configuration not compiled in (e.g. N > 16) */
+#define P2PMG_E_UNSUPPORTED 5 /* configuration not supported (e.g. N > 64) */
 
 /* Q-table element type: f64 = the reference's np.zeros table (rl.py:73), bit-exact;
  * f32 = throughput mode (TD update in f32, held to 1e-5 relative). */
@@ -77,8 +77,8 @@ typedef struct p2pmg_ctx p2pmg_ctx;
 
 typedef struct p2pmg_config {
   int32_t n_scenarios;      /* S */
-  int32_t n_agents;         /* N agents per scenario (1..16) */
-  int32_t rounds;           /* R: negotiation runs R+1 rounds (community.py:75), R <= 7 */
+  int32_t n_agents;         /* N agents per scenario, 1..64 (a scenario is one 64-lane wave) */
+  int32_t rounds;           /* R >= 0: negotiation runs R+1 rounds (community.py:75); R + 1 <= 4096 */
   int32_t horizon;          /* T timesteps per episode */
   int32_t q_dtype;          /* P2PMG_Q_F64 | P2PMG_Q_F32 */
   int32_t n_time_states;    /* 20 (agent.py:258-261) */
@@ -152,6 +152,9 @@ typedef struct p2pmg_episode_args {
 /* next_epsilon holds the caller's guess as given, 0.0 included (DQN-style schedules decay to 0).
  * Without this flag only a positive next_epsilon is a guess; anything else means "same epsilon". */
 #define P2PMG_FLAG_NEXT_EPSILON 16
+/* The general kernel's LDS-tile form (the scenario's P in two LDS tiles, any N <= 64; the form every
+ * N outside {1..8, 16} runs) at any N: the cross-check of the register form, same results bit for bit. */
+#define P2PMG_FLAG_TILE_KERNEL 32
 
 /* version / defaults */
 int p2pmg_abi_version(void);

@@ -38,7 +38,7 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-KERNEL_PARTS = 9  # p2pmg_kernels.hip is compiled once per part (-DP2PMG_PART=k), see its header
+KERNEL_PARTS = 11  # p2pmg_kernels.hip is compiled once per part (-DP2PMG_PART=k), see its header
 # Per-part compiler flags.  Part 5 (episode_sq16_kernel, VALU-issue-bound) without the SLP vectorizer:
 # SLP packs adjacent f32 adds / muls into v_pk_add_f32 / v_pk_mul_f32, which issue at 6.6 SIMD cycles
 # against 2 x 2.9 / 2 x 2.6 for the scalar pair at 4 waves per SIMD (profiles/r04_ubench_rate.jsonl);
@@ -51,7 +51,7 @@ PART_FLAGS = {5: ["-fno-slp-vectorize"]}
 def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=(), jobs: int = 0) -> str:
     """defines: extra -D flags, or raw compiler flags when they start with "-" (timing-only ablation
     builds go to a different ``out``).
-    The translation units (9 parts of p2pmg_kernels.hip, p2pmg_dqn.hip, p2pmg_runtime.cpp) compile
+    The translation units (11 parts of p2pmg_kernels.hip, p2pmg_dqn.hip, p2pmg_runtime.cpp) compile
     in parallel into build/obj/<tag>/, then link into one shared library.  An exclusive file lock
     per tag serialises concurrent builders (torchrun ranks, pytest-xdist workers that all find the
     sources newer): the later ones wait, see a fresh library and return without compiling."""

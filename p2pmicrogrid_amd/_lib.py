@@ -65,7 +65,7 @@ class DqnConfig(C.Structure):
                 ("capacity", C.c_int32), ("agents_per_block", C.c_int32), ("grad_segments", C.c_int32)]
 
 
-ABI_VERSION = 7  # include/p2pmg.h P2PMG_ABI_VERSION
+ABI_VERSION = 8  # include/p2pmg.h P2PMG_ABI_VERSION
 
 # p2pmg_exchange_fn: int (*)(void* user, float* segments, int64_t floats_per_rank, int rank, int nranks)
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_int64, C.c_int, C.c_int)
@@ -78,6 +78,7 @@ class EpisodeArgs(C.Structure):
 
 
 FLAG_PHILOX_PREPASS, FLAG_PHILOX_INKERNEL, FLAG_GENERAL_KERNEL, FLAG_RESET_T0, FLAG_NEXT_EPSILON = 1, 2, 4, 8, 16
+FLAG_TILE_KERNEL = 32
 
 
 class P2PMGError(RuntimeError):

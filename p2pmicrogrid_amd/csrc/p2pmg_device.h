@@ -92,20 +92,37 @@ __device__ __forceinline__ uint32_t philox_block_codes(uint32_t blk, uint32_t ep
   return decision_code(c0, a0, thr, all) | (decision_code(c1, a1, thr, all) << 8) |
          (decision_code(c2, a2, thr, all) << 16) | (decision_code(c3, a3, thr, all) << 24);
 }
-// every round's code of step t, byte r (bytes r >= R1: 255); R1 <= 8
+// the codes of rounds 0 .. min(R1, 8) - 1 of step t, byte r (bytes r >= R1: 255); rounds 8 and up
+// (R1 > 8) come from philox_round_code one at a time
 __device__ __forceinline__ uint64_t philox_step_codes(int t, int R1, uint32_t episode, uint32_t gid, uint32_t thr,
                                                       int all, uint32_t k0, uint32_t k1) {
-  const uint32_t kf = (uint32_t)t * (uint32_t)R1, kl = kf + (uint32_t)R1 - 1u;
+  const int R8 = R1 < 8 ? R1 : 8;
+  const uint32_t kf = (uint32_t)t * (uint32_t)R1, kl = kf + (uint32_t)R8 - 1u;
   uint64_t out = ~0ull;
   for (uint32_t b = kf >> 2; b <= (kl >> 2); ++b) {
     const uint32_t c4 = philox_block_codes(b, episode, gid, thr, all, k0, k1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = (int)(4u * b + (uint32_t)j) - (int)kf;
-      if (r >= 0 && r < R1) out = (out & ~(0xFFull << (8 * r))) | ((uint64_t)((c4 >> (8 * j)) & 0xFFu) << (8 * r));
+      if (r >= 0 && r < R8) out = (out & ~(0xFFull << (8 * r))) | ((uint64_t)((c4 >> (8 * j)) & 0xFFu) << (8 * r));
     }
   }
   return out;
+}
+// the code of round r (any r < R1) of step t: byte k % 4 of block k / 4, k = t R1 + r
+__device__ __forceinline__ uint32_t philox_round_code(int t, int R1, int r, uint32_t episode, uint32_t gid,
+                                                      uint32_t thr, int all, uint32_t k0, uint32_t k1) {
+  const uint32_t k = (uint32_t)t * (uint32_t)R1 + (uint32_t)r;
+  return (philox_block_codes(k >> 2, episode, gid, thr, all, k0, k1) >> (8 * (k & 3u))) & 0xFFu;
+}
+// code word w of step t (rounds 4w .. 4w + 3, byte b = round 4w + b, 255 past R1): the pre-passes'
+// words w >= 2 (the 64-bit step codes cover words 0 and 1)
+__device__ __forceinline__ uint32_t philox_code_word(int t, int R1, int w, uint32_t episode, uint32_t gid,
+                                                     uint32_t thr, int all, uint32_t k0, uint32_t k1) {
+  uint32_t word = 0xFFFFFFFFu;
+  for (int b = 0; b < 4 && 4 * w + b < R1; ++b)
+    word = (word & ~(0xFFu << (8 * b))) | (philox_round_code(t, R1, 4 * w + b, episode, gid, thr, all, k0, k1) << (8 * b));
+  return word;
 }
 
 // RuleAgent._update_storage (agent.py:138-153) with BatteryStorage bookkeeping (storage.py:79-100),

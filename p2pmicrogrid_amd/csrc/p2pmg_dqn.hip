@@ -123,16 +123,33 @@ __global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
 }
 
 // ----------------------------------------------------------------- act: one env step
-template <int N>
-__global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
+// dqn_act_kernel<NC, WIDE>: one workgroup per scenario.  WIDE = false: NC = N agents compiled in
+// (N <= 16), one wave per agent.  WIDE = true: any n = p.N <= NC (the community sizes 9..15 and
+// 17..64), NW = 16 waves, wave w acting for agents w, w + 16, ... in turn in each round
+// (a round is Jacobi: every agent reads the previous round's P, community.py:84-86, so the order of
+// the agents within a round does not matter).  Both forms sum over j = 0..n-1 in order and divide
+// by n as IEEE quotients: the same bits.
+template <int NC, bool WIDE>
+constexpr int dqn_act_waves() {
+  return WIDE ? 16 : NC;
+}
+template <int NC, bool WIDE>
+__global__ __launch_bounds__((dqn_act_waves<NC, WIDE>() * kWave)) void dqn_act_kernel(const DqnParams d) {
+  constexpr int NW = dqn_act_waves<NC, WIDE>();  // waves
+  constexpr int APW = (NC + NW - 1) / NW;    // agents per wave
   const EpisodeParams& p = d.e;
-  __shared__ float shP[2][N * N];
-  __shared__ float4 shH[N][kH];
-  __shared__ float shR[N];
+  __shared__ float shP[2][NC * NC];
+  __shared__ float4 shH[NW][kH];
+  __shared__ float shR[NC];
+  const int n = WIDE ? p.N : NC;
+  const float nf = (float)n;
+  auto divn = [&](float x) -> float {
+    if constexpr (WIDE) return x / nf;
+    else return div_n<NC>(x);
+  };
   const int s = blockIdx.x;
-  const int i = threadIdx.x / kWave;
+  const int w = threadIdx.x / kWave;
   const int lane = threadIdx.x % kWave;
-  const int a = s * N + i;
   const int t = d.t, T = p.T, tn = (t + 1 == T) ? 0 : t + 1;
   const int R1 = p.R + 1, W = (R1 + 3) >> 2;
   const size_t A = (size_t)p.A;
@@ -141,158 +158,203 @@ __global__ __launch_bounds__(N * kWave) void dqn_act_kernel(const DqnParams d) {
   const float* e1 = p.env + ((size_t)tn * p.n_env + s_env) * kEnvStride;
   const float time_t = e0[0], t_out = e0[1], buy = e0[2], inj = e0[3], p2pp = e0[4];
   const float time_n = e1[0];
-  const float2 f0 = p.prof[(size_t)t * A + a], f1 = p.prof[(size_t)tn * A + a];
-  const float mi = p.max_in[a];
-  float tin = p.t_in[a], tm = p.t_m[a];
-  const float bal = (f0.x - f0.y) / mi;  // RLAgent._get_balance agent.py:172-176
-  const float baln = (f1.x - f1.y) / mi;
-  const float tnorm = (tin - p.setpoint) / p.margin;  // HPHeating.normalized_temperature heating.py:118-120
-  const float4 lv = p.hp_lv[a];
-  const float* th = d.theta + (size_t)(d.n_nets == 1 ? 0 : a) * kNetStride;
-  // this lane's hidden unit (rl.py:139-141): first-layer column, biases, output weight
-  const float w10 = th[kOffW1 + 0 * kH + lane], w11 = th[kOffW1 + 1 * kH + lane], w12 = th[kOffW1 + 2 * kH + lane],
-              w13 = th[kOffW1 + 3 * kH + lane], w14 = th[kOffW1 + 4 * kH + lane];
-  const float b1 = th[kOffB1 + lane], b2 = th[kOffB2 + lane], w3 = th[kOffW3 + lane], b3 = th[kOffB3];
-  const float* w2col = th + kOffW2 + lane;
   const bool greedy_mode = p.mode == 1;
+  // the wave's agents: wave-uniform scalars (registers for one agent per wave, LDS for several) and
+  // this lane's hidden unit of the agent's network (rl.py:139-141): first-layer column, biases,
+  // output weight (registers for one agent per wave, read where used for several: L2 hits)
+  struct Ag {
+    int a;
+    float mi, tin, tm, bal, baln, tnorm;
+    float4 lv;
+    int act;
+    float hp, p2pf;
+  };
+  struct Unit {
+    float w10, w11, w12, w13, w14, b1, b2, w3, b3;
+    const float* w2col;
+  };
+  auto load_unit = [&](int a) -> Unit {
+    const float* th = d.theta + (size_t)(d.n_nets == 1 ? 0 : a) * kNetStride;
+    return Unit{th[kOffW1 + 0 * kH + lane], th[kOffW1 + 1 * kH + lane], th[kOffW1 + 2 * kH + lane],
+                th[kOffW1 + 3 * kH + lane], th[kOffW1 + 4 * kH + lane], th[kOffB1 + lane],
+                th[kOffB2 + lane],          th[kOffW3 + lane],          th[kOffB3],
+                th + kOffW2 + lane};
+  };
+  __shared__ Ag sAg[WIDE ? NC : 1];
+  Ag rAg;
+  auto agent = [&](int i) -> Ag& {
+    if constexpr (WIDE) return sAg[i];
+    else return rAg;
+  };
+  Unit ru{};
+  for (int k = 0; k < APW; ++k) {
+    const int i = w + k * NW;
+    if (i >= n) break;  // wave-uniform
+    Ag& g = agent(i);
+    g.a = s * n + i;
+    const float2 f0 = p.prof[(size_t)t * A + g.a], f1 = p.prof[(size_t)tn * A + g.a];
+    g.mi = p.max_in[g.a];
+    g.tin = p.t_in[g.a];
+    g.tm = p.t_m[g.a];
+    g.bal = (f0.x - f0.y) / g.mi;  // RLAgent._get_balance agent.py:172-176
+    g.baln = (f1.x - f1.y) / g.mi;
+    g.tnorm = (g.tin - p.setpoint) / p.margin;  // HPHeating.normalized_temperature heating.py:118-120
+    g.lv = p.hp_lv[g.a];
+    g.act = 0;
+    g.hp = 0.0f;
+    g.p2pf = 0.0f;
+    if constexpr (!WIDE) ru = load_unit(g.a);
+  }
 
-  if (threadIdx.x < N * N) shP[0][threadIdx.x] = 0.0f;
+  if (threadIdx.x < NC * NC) shP[0][threadIdx.x] = 0.0f;
   __syncthreads();
-  int cur = 0, act = 0;
-  float hp = 0.0f, p2pf = 0.0f;
+  int cur = 0;
   for (int r = 0; r < R1; ++r) {
     const float* P = shP[cur];
-    // powers = -P[:, i], diagonal zeroed (community.py:76,81); p2p = mean / max_in (agent.py:203)
-    float acc = 0.0f;
+    for (int k = 0; k < APW; ++k) {
+      const int i = w + k * NW;
+      if (i >= n) break;  // wave-uniform
+      Ag& g = agent(i);
+      const int a = g.a;
+      // powers = -P[:, i], diagonal zeroed (community.py:76,81); p2p = mean / max_in (agent.py:203)
+      float acc = 0.0f;
 #pragma unroll
-    for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : P[j * N + i]));
-    p2pf = div_n<N>(acc) / mi;
-    int code = 255;  // ActorModel.select_action rl.py:174-183: explore draw, else greedy
-    if (!greedy_mode) {
-      if (p.rng == 0) {
-        code = (int)((p.codes[((size_t)t * W + (r >> 2)) * A + a] >> (8 * (r & 3))) & 0xFFu);
-      } else {
-        // word k = t (R + 1) + r of the agent's decision stream (p2pmg_device.h, oracle/philox.py::decision_draws)
-        const uint32_t k = (uint32_t)t * (uint32_t)R1 + (uint32_t)r;
-        code = (int)((philox_block_codes(k >> 2, (uint32_t)p.episode, p.agent_offset + (uint32_t)a, p.eps_thr, p.eps_all,
-                                         p.seed_lo, p.seed_hi) >> (8 * (k & 3u))) & 0xFFu);
+      for (int j = 0; j < n; ++j) acc = acc + (-((j == i) ? 0.0f : P[j * n + i]));
+      g.p2pf = divn(acc) / g.mi;
+      int code = 255;  // ActorModel.select_action rl.py:174-183: explore draw, else greedy
+      if (!greedy_mode) {
+        if (p.rng == 0) {
+          code = (int)((p.codes[((size_t)t * W + (r >> 2)) * A + a] >> (8 * (r & 3))) & 0xFFu);
+        } else {
+          // word k = t (R + 1) + r of the agent's decision stream (p2pmg_device.h, oracle/philox.py::decision_draws)
+          code = (int)philox_round_code(t, R1, r, (uint32_t)p.episode, p.agent_offset + (uint32_t)a, p.eps_thr,
+                                        p.eps_all, p.seed_lo, p.seed_hi);
+        }
       }
-    }
-    if (code == 255) {
-      // ActorModel.greedy_action rl.py:188-196: Q(obs, a) for a in (0, .5, 1), argmax (first max)
-      float z = p2pf * w13;
-      z = fmaf(bal, w12, z);
-      z = fmaf(tnorm, w11, z);
-      z = fmaf(time_t, w10, z);
-      const float h0 = relu(z + b1), h1 = relu(fmaf(0.5f, w14, z) + b1), h2 = relu((z + w14) + b1);
-      shH[i][lane] = make_float4(h0, h1, h2, 0.0f);
-      wave_lds_fence();
-      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+      if (code == 255) {
+        // ActorModel.greedy_action rl.py:188-196: Q(obs, a) for a in (0, .5, 1), argmax (first max)
+        const Unit u = WIDE ? load_unit(a) : ru;
+        float z = g.p2pf * u.w13;
+        z = fmaf(g.bal, u.w12, z);
+        z = fmaf(g.tnorm, u.w11, z);
+        z = fmaf(time_t, u.w10, z);
+        const float h0 = relu(z + u.b1), h1 = relu(fmaf(0.5f, u.w14, z) + u.b1), h2 = relu((z + u.w14) + u.b1);
+        shH[w][lane] = make_float4(h0, h1, h2, 0.0f);
+        wave_lds_fence();
+        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
 #pragma unroll 8
-      for (int k = 0; k < kH; ++k) {
-        const float wk = w2col[k * kH];
-        const float4 hk = shH[i][k];
-        a0 = fmaf(hk.x, wk, a0);
-        a1 = fmaf(hk.y, wk, a1);
-        a2 = fmaf(hk.z, wk, a2);
+        for (int kk = 0; kk < kH; ++kk) {
+          const float wk = u.w2col[kk * kH];
+          const float4 hk = shH[w][kk];
+          a0 = fmaf(hk.x, wk, a0);
+          a1 = fmaf(hk.y, wk, a1);
+          a2 = fmaf(hk.z, wk, a2);
+        }
+        wave_lds_fence();
+        const float q0 = wave_sum(relu(a0 + u.b2) * u.w3) + u.b3;
+        const float q1 = wave_sum(relu(a1 + u.b2) * u.w3) + u.b3;
+        const float q2 = wave_sum(relu(a2 + u.b2) * u.w3) + u.b3;
+        g.act = 0;
+        float best = q0;
+        if (q1 > best) { best = q1; g.act = 1; }
+        if (q2 > best) g.act = 2;
+      } else {
+        g.act = code;
       }
-      wave_lds_fence();
-      const float q0 = wave_sum(relu(a0 + b2) * w3) + b3;
-      const float q1 = wave_sum(relu(a1 + b2) * w3) + b3;
-      const float q2 = wave_sum(relu(a2 + b2) * w3) + b3;
-      act = 0;
-      float best = q0;
-      if (q1 > best) { best = q1; act = 1; }
-      if (q2 > best) act = 2;
-    } else {
-      act = code;
-    }
-    hp = act == 0 ? lv.x : (act == 1 ? lv.y : lv.z);  // heating.set_power(action) -> hp.power * max_power
-    // RLAgent._divide_power agent.py:186-195 on out = balance * max_in + hp (agent.py:210)
-    const float out = (bal * mi) + hp;
-    const float so = sgn(out);
-    float tot = 0.0f, fj = 0.0f;
+      g.hp = g.act == 0 ? g.lv.x : (g.act == 1 ? g.lv.y : g.lv.z);  // heating.set_power(action) -> hp.power * max_power
+      // RLAgent._divide_power agent.py:186-195 on out = balance * max_in + hp (agent.py:210)
+      const float out = (g.bal * g.mi) + g.hp;
+      const float so = sgn(out);
+      float tot = 0.0f, fj = 0.0f;
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const float pw = -((j == i || r == 0) ? 0.0f : P[j * N + i]);
-      const float f = (so != sgn(pw)) ? pw : 0.0f;
-      tot = tot + f;
-      if (j == lane) fj = f;
+      for (int j = 0; j < n; ++j) {
+        const float pw = -((j == i || r == 0) ? 0.0f : P[j * n + i]);
+        const float f = (so != sgn(pw)) ? pw : 0.0f;
+        tot = tot + f;
+        if (j == lane) fj = f;
+      }
+      tot = fabsf(tot);
+      if (lane < n) {
+        float v;
+        if (tot == 0.0f) v = divn(out * 1.0f);
+        else v = (lane == i) ? (tot == tot ? out * 0.0f : tot) : (out * fabsf(fj)) / tot;
+        shP[cur ^ 1][i * n + lane] = v;
+      }
+      if (lane == 0 && (p.record & 32)) p.rec_action[((size_t)t * R1 + r) * A + a] = (uint8_t)g.act;
     }
-    tot = fabsf(tot);
-    if (lane < N) {
-      float v;
-      if (tot == 0.0f) v = div_n<N>(out * 1.0f);
-      else v = (lane == i) ? (tot == tot ? out * 0.0f : tot) : (out * fabsf(fj)) / tot;
-      shP[cur ^ 1][i * N + lane] = v;
-    }
-    if (lane == 0 && (p.record & 32)) p.rec_action[((size_t)t * R1 + r) * A + a] = (uint8_t)act;
     __syncthreads();
     cur ^= 1;
   }
-  // CommunityMicrogrid._assign_powers community.py:45-54 (final P, diagonal kept)
   const float* P = shP[cur];
-  float g = 0.0f, pp = 0.0f;
+  for (int k = 0; k < APW; ++k) {
+    const int i = w + k * NW;
+    if (i >= n) break;  // wave-uniform
+    Ag& g = agent(i);
+    const int a = g.a;
+    // CommunityMicrogrid._assign_powers community.py:45-54 (final P, diagonal kept)
+    float gg = 0.0f, pp = 0.0f;
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
-    const float pij = P[i * N + j], pji = P[j * N + i];
-    const float ex = __builtin_amdgcn_fmed3f(pij, -pji, 0.0f);  // pair_exchange (p2pmg_kernels.hip)
-    g = g + (pij - ex);
-    pp = pp + ex;
-  }
-  // _compute_costs community.py:56-65; RLAgent.get_reward agent.py:225-232 (pre-update T_in)
-  float cost = (g >= 0.0f) ? g * buy : g * inj;
-  cost = cost + pp * p2pp;
-  cost = (cost * p.slot) / p.mph;
-  cost = cost * p.kilo;
-  float pen = fmaxf(fmaxf(0.0f, p.lower - tin), fmaxf(0.0f, tin - p.upper));
-  pen = pen > 0.0f ? pen + 1.0f : 0.0f;
-  const float rw = -(cost + p.penw * pen);
-
-  if (p.mode != 1) {
-    // DQNAgent.save_memory agent.py:332-336 -> ReplayBuffer.add rl.py:208-212
-    const int32_t n_added = d.added[a];
-    float* slot = d.buf + ((size_t)a * d.cap + (size_t)(n_added % d.cap)) * kTrans;
-    if (lane < kTrans) {
-      const float av = act == 0 ? 0.0f : (act == 1 ? 0.5f : 1.0f);
-      float v;
-      switch (lane) {
-        case 0: v = time_t; break;
-        case 1: v = tnorm; break;
-        case 2: v = bal; break;
-        case 3: v = p2pf; break;
-        case 4: v = av; break;
-        case 5: v = rw; break;
-        case 6: v = time_n; break;
-        case 7: v = tnorm; break;  // next state: same (pre-update) temperature (community.py:161)
-        case 8: v = baln; break;
-        default: v = 0.0f / mi; break;  // next state p2p = mean(zeros) / max_in
-      }
-      slot[lane] = v;
+    for (int j = 0; j < n; ++j) {
+      const float pij = P[i * n + j], pji = P[j * n + i];
+      const float ex = __builtin_amdgcn_fmed3f(pij, -pji, 0.0f);  // pair_exchange (p2pmg_kernels.hip)
+      gg = gg + (pij - ex);
+      pp = pp + ex;
     }
-    if (lane == 0) d.added[a] = n_added + 1;
-    // Trainer.train -> ReplayBuffer.sample_batch (rl.py:299-305, 226-241) right after the append
-    // (agent.py:338-342): the same wave draws the agent's 32 slots, no separate launch
-    if (p.mode == 0 && d.fused_sample) sample_slots(d, a, lane, n_added + 1);
-  }
-  if (lane == 0) {
-    const size_t k = (size_t)t * A + a;
-    if (p.record & 1) p.rec_reward[k] = rw;
-    if (p.record & 2) p.rec_cost[k] = cost;
-    if (p.record & 4) p.rec_grid[k] = g;
-    if (p.record & 8) p.rec_p2p[k] = pp;
-    if (p.record & 16) p.rec_tin[k] = tin;
-    rc_update(p, t_out, hp, tin, tm);  // HPHeating.step heating.py:138-143
-    p.t_in[a] = tin;
-    p.t_m[a] = tm;
-    shR[i] = rw;
+    // _compute_costs community.py:56-65; RLAgent.get_reward agent.py:225-232 (pre-update T_in)
+    float cost = (gg >= 0.0f) ? gg * buy : gg * inj;
+    cost = cost + pp * p2pp;
+    cost = (cost * p.slot) / p.mph;
+    cost = cost * p.kilo;
+    float pen = fmaxf(fmaxf(0.0f, p.lower - g.tin), fmaxf(0.0f, g.tin - p.upper));
+    pen = pen > 0.0f ? pen + 1.0f : 0.0f;
+    const float rw = -(cost + p.penw * pen);
+
+    if (p.mode != 1) {
+      // DQNAgent.save_memory agent.py:332-336 -> ReplayBuffer.add rl.py:208-212
+      const int32_t n_added = d.added[a];
+      float* slot = d.buf + ((size_t)a * d.cap + (size_t)(n_added % d.cap)) * kTrans;
+      if (lane < kTrans) {
+        const float av = g.act == 0 ? 0.0f : (g.act == 1 ? 0.5f : 1.0f);
+        float v;
+        switch (lane) {
+          case 0: v = time_t; break;
+          case 1: v = g.tnorm; break;
+          case 2: v = g.bal; break;
+          case 3: v = g.p2pf; break;
+          case 4: v = av; break;
+          case 5: v = rw; break;
+          case 6: v = time_n; break;
+          case 7: v = g.tnorm; break;  // next state: same (pre-update) temperature (community.py:161)
+          case 8: v = g.baln; break;
+          default: v = 0.0f / g.mi; break;  // next state p2p = mean(zeros) / max_in
+        }
+        slot[lane] = v;
+      }
+      if (lane == 0) d.added[a] = n_added + 1;
+      // Trainer.train -> ReplayBuffer.sample_batch (rl.py:299-305, 226-241) right after the append
+      // (agent.py:338-342): the same wave draws the agent's 32 slots, no separate launch
+      if (p.mode == 0 && d.fused_sample) sample_slots(d, a, lane, n_added + 1);
+    }
+    if (lane == 0) {
+      const size_t kr = (size_t)t * A + a;
+      if (p.record & 1) p.rec_reward[kr] = rw;
+      if (p.record & 2) p.rec_cost[kr] = cost;
+      if (p.record & 4) p.rec_grid[kr] = gg;
+      if (p.record & 8) p.rec_p2p[kr] = pp;
+      if (p.record & 16) p.rec_tin[kr] = g.tin;
+      float tin = g.tin, tm = g.tm;
+      rc_update(p, t_out, g.hp, tin, tm);  // HPHeating.step heating.py:138-143
+      p.t_in[a] = tin;
+      p.t_m[a] = tm;
+      shR[i] = rw;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {  // avg_reward = sum_t mean_i r (community.py:179), canonical order
     float m = 0.0f;
 #pragma unroll
-    for (int j = 0; j < N; ++j) m = m + shR[j];
-    const float ep = (t == 0 ? 0.0f : d.ep_acc[s]) + div_n<N>(m);
+    for (int j = 0; j < n; ++j) m = m + shR[j];
+    const float ep = (t == 0 ? 0.0f : d.ep_acc[s]) + divn(m);
     d.ep_acc[s] = ep;
     p.ep_reward[s] = ep;
   }
@@ -410,10 +472,10 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
   const float b3 = th[kOffB3];
   // every round's exploration draw (or replayed code) ahead of the rounds: they depend only on
   // (t, episode, agent), so they run under the prologue's load latency, off the rounds' chain
-  uint64_t codes_pack = ~0ull;  // byte r: code of round r (255 = greedy); R + 1 <= kMaxRounds1 = 8 (p2pmg_create)
+  uint64_t codes_pack = ~0ull;  // byte r: code of round r < 8 (255 = greedy); later rounds are drawn in the loop
   if (agent_thr && !greedy_mode) {
     if (p.rng == 0) {
-      for (int w4 = 0; w4 < W; ++w4)
+      for (int w4 = 0; w4 < W && w4 < 2; ++w4)
         codes_pack = (codes_pack & ~(0xFFFFFFFFull << (32 * w4))) |
                      ((uint64_t)p.codes[((size_t)t * W + w4) * A + a] << (32 * w4));
     } else {
@@ -443,7 +505,13 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
       for (int jj = 0; jj < N; ++jj) acc = acc + (-((jj == i) ? 0.0f : P[jj * N + i]));
       p2pf = div_n<N>(acc) / mi;
       code = 255;  // ActorModel.select_action rl.py:174-183: explore draw, else greedy
-      if (!greedy_mode) code = (int)((codes_pack >> (8 * r)) & 0xFFu);
+      if (!greedy_mode) {
+        if (r < 8) code = (int)((codes_pack >> (8 * r)) & 0xFFu);
+        else if (p.rng == 0) code = (int)((p.codes[((size_t)t * W + (r >> 2)) * A + a] >> (8 * (r & 3))) & 0xFFu);
+        else
+          code = (int)philox_round_code(t, R1, r, (uint32_t)p.episode, p.agent_offset + (uint32_t)a, p.eps_thr,
+                                        p.eps_all, p.seed_lo, p.seed_hi);
+      }
       greedy = code == 255;
       shX[j] = make_float4(time_t, tnorm, bal, p2pf);
     }
@@ -1241,7 +1309,9 @@ __global__ void dqn_forward_kernel(const float* __restrict__ th, int n, const fl
 }  // namespace
 
 hipError_t launch_dqn_act(const DqnParams& d, hipStream_t st) {
-  if (d.n_nets == 1 && !d.act_wave) {  // one shared network: AGW agents per workgroup on MFMA tiles
+  // sizes the MFMA act kernel is built for (its action records pack 8 rounds)
+  const bool mfma_n = ((d.e.N >= 1 && d.e.N <= 8) || d.e.N == 16) && d.e.R + 1 <= 8;
+  if (d.n_nets == 1 && !d.act_wave && mfma_n) {  // one shared network: AGW agents per workgroup on MFMA tiles
     // AGW = 16 agent slots per workgroup (default), or 8 (d.act_agw, P2PMG_ACT_AGW=8: more, shorter
     // workgroups; N <= 8 only) -- the same results bit for bit
     switch (d.e.N) {
@@ -1264,14 +1334,20 @@ hipError_t launch_dqn_act(const DqnParams& d, hipStream_t st) {
     }
     return hipGetLastError();
   }
-  const dim3 grid(d.e.S);
+  const dim3 grid(d.e.S), wide(16 * kWave), wide64(dqn_act_waves<64, true>() * kWave);
   switch (d.e.N) {
 #define P2PMG_DQN_ACT(NN) \
-  case NN: hipLaunchKernelGGL(dqn_act_kernel<NN>, grid, dim3(NN * kWave), 0, st, d); break;
+  case NN: hipLaunchKernelGGL((dqn_act_kernel<NN, false>), grid, dim3(NN * kWave), 0, st, d); break;
     P2PMG_DQN_ACT(1) P2PMG_DQN_ACT(2) P2PMG_DQN_ACT(3) P2PMG_DQN_ACT(4) P2PMG_DQN_ACT(5) P2PMG_DQN_ACT(6)
     P2PMG_DQN_ACT(7) P2PMG_DQN_ACT(8) P2PMG_DQN_ACT(16)
 #undef P2PMG_DQN_ACT
-    default: return hipErrorInvalidValue;
+    default: {  // every other community size: wave w acts for agents w, w + NW, ...
+      const int nc = general_tile_cap(d.e.N);
+      if (d.e.N < 1 || d.e.N > kMaxAgents) return hipErrorInvalidValue;
+      if (nc == 16) hipLaunchKernelGGL((dqn_act_kernel<16, true>), grid, wide, 0, st, d);
+      else if (nc == 32) hipLaunchKernelGGL((dqn_act_kernel<32, true>), grid, wide, 0, st, d);
+      else hipLaunchKernelGGL((dqn_act_kernel<64, true>), grid, wide64, 0, st, d);
+    }
   }
   return hipGetLastError();
 }

@@ -9,8 +9,12 @@ namespace p2pmg {
 constexpr int kEnvStride = 8;  // floats per env row: time, t_out, buy, inj, p2p, pad x3
 constexpr int kQPad = 4;       // Q row padded to 4 actions: 32-B (f64) / 16-B (f32) aligned rows
 constexpr int kWave = 64;      // one wave per workgroup
-constexpr int kMaxAgents = 16; // compiled-in agents per scenario
-constexpr int kMaxRounds1 = 8; // R + 1 <= 8 (two code words)
+constexpr int kMaxAgents = 64;  // agents per scenario: one 64-lane wave holds a scenario (general kernel)
+// R + 1 rounds: no kernel limit (rounds 8 and above read their codes per round); the bound only keeps
+// the per-step code and record arrays ([T][ceil((R+1)/4)][A], [T][R+1][A]) in 32-bit row counts
+constexpr int kMaxRounds1 = 4096;
+// capacity of the general kernel's LDS-tile form for n agents (16, 32 or 64)
+inline constexpr int general_tile_cap(int n) { return n <= 16 ? 16 : (n <= 32 ? 32 : 64); }
 constexpr double kDeltaScale = 1099511627776.0;  // 2^40: shared-table TD deltas in int64 fixed point
 // shared-table delta replicas: workgroup b accumulates into copy (b % 8), i.e. its own XCD\'s copy
 // (blocks are dealt round-robin over the 8 XCDs); the copies are folded before use
@@ -131,7 +135,8 @@ struct RcParams {
   float inv_ci, inv_cm, inv_ri, inv_re, inv_rvent, c_in, c_m, solar, cop, spm, slot;
 };
 
-hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream);
+// tile != 0: the LDS-tile form at any N (else registers for N in {1..8, 16}, tiles for the rest)
+hipError_t launch_episode(const EpisodeParams& p, int q_dtype, int tile, hipStream_t stream);
 // fast per-agent-table path: step pre-pass ([T][A] {balw, bins}; optionally the Philox code
 // words) + episode_fast_kernel (N <= 8, R + 1 <= 4, no battery, no shared table)
 // Where one step pre-pass writes: its buffers and the episode its Philox draws are for.
@@ -176,6 +181,8 @@ P2PMG_DECL_FAST_PART(4)
 hipError_t launch_general_part6(const EpisodeParams& p, int q_dtype, hipStream_t stream);
 hipError_t launch_general_part7(const EpisodeParams& p, int q_dtype, hipStream_t stream);
 hipError_t launch_general_part8(const EpisodeParams& p, int q_dtype, hipStream_t stream);
+hipError_t launch_tile_part9(const EpisodeParams& p, int q_dtype, int nc, hipStream_t stream);
+hipError_t launch_tile_part10(const EpisodeParams& p, int q_dtype, int nc, hipStream_t stream);
 // RuleAgent community run (R = 0): rule_episode_kernel; hp_on [A] hysteresis state in/out
 hipError_t launch_rule_episode(const EpisodeParams& p, float* hp_on, hipStream_t stream);
 // shared table, N = 16, R <= 1 (configs[2]): episode_sq16_kernel; records packed like the fast path

@@ -17,6 +17,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "p2pmg_internal.h"
 
@@ -24,6 +25,7 @@
 // a disjoint subset of the launchers below, so each template kernel is instantiated in one part only.
 //   0: small kernels + dispatchers   1-4: episode_fast_kernel, N = 1-2 / 3-4 / 5-6 / 7-8
 //   5: episode_sq16_kernel           6-8: episode_kernel, N = 1-4 / 5-8 / 16
+//   9-10: episode_kernel's LDS-tile form, up to 16 / 32 and 64 agents
 // Without -DP2PMG_PART everything is in one translation unit.
 #ifndef P2PMG_PART
 #define P2PMG_PART -1
@@ -472,13 +474,83 @@ __device__ __forceinline__ Row4<QT> gather_row(const QT* p) {
   return load_row(p);
 #endif
 }
-template <int N, typename QT, bool B20, bool SQ>
-__global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(const EpisodeParams p) {
-  constexpr int G = pow2ceil(N);
+// The proposal matrix P of one scenario as the general kernel holds it (community.py:75-86): lane i
+// owns row i; round r reads column i of round r - 1's P (Jacobi: every agent answers the previous
+// round's proposals) and writes its new row; the market reads row i and column i of the final P.
+//   PRegs<N>  N <= 16 compiled in: row and column in registers, the column by exchange<N>
+//   PTile<NC> any community size n <= NC (16, 32, 64) at run time: the scenario's P in two LDS
+//             tiles (the round being read, the round being written) with an odd row stride, so the
+//             column read (lane i at j * stride + i) and the row read (lane i at i * stride + j) are
+//             both conflict-free.  Every agent of a scenario is a lane of the same wave, so a
+//             wavefront-scope fence orders the tiles (no workgroup barrier, no vmcnt drain).
+template <int N>
+struct PRegs {
+  float row[N], col[N];
+  float* sh;
+  int i, sl;
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (int j = 0; j < N; ++j) { row[j] = 0.0f; col[j] = 0.0f; }
+  }
+  __device__ __forceinline__ void next_round() { exchange<N>(row, col, i, sl, sh); }
+  __device__ __forceinline__ float colv(int j) const { return col[j]; }
+  __device__ __forceinline__ float rowv(int j) const { return row[j]; }
+  __device__ __forceinline__ void put(int j, float v) { row[j] = v; }
+};
+template <int NC>
+struct PTile {
+  static constexpr int kStride = NC + 1;
+  static constexpr int kTile = NC * kStride;
+  float* base;  // this scenario's two tiles
+  int i, rd, wr;
+  __device__ __forceinline__ void clear() {}  // round 0 reads no column (its powers are all -0)
+  __device__ __forceinline__ void next_round() {
+    wave_lds_fence();  // every lane's row of the round just written is visible
+    rd = wr;
+    wr ^= 1;
+  }
+  __device__ __forceinline__ float colv(int j) const { return base[rd * kTile + j * kStride + i]; }
+  __device__ __forceinline__ float rowv(int j) const { return base[rd * kTile + i * kStride + j]; }
+  __device__ __forceinline__ void put(int j, float v) { base[wr * kTile + i * kStride + j] = v; }
+};
+// sum_{k < n} v_k over a scenario group of run-time size n through LDS, sequential from +0.0
+template <int NC>
+__device__ __forceinline__ float group_sum_n(float v, int i, int sl, int n, float* sh) {
+  if (i < n) sh[sl * NC + i] = v;
+  wave_lds_fence();
+  float m = 0.0f;
+  for (int k = 0; k < n; ++k) m = m + sh[sl * NC + k];
+  wave_lds_fence();
+  return m;
+}
+// exploration code of round r >= 8 of step t (the 64-bit code word holds rounds 0..7): the replay
+// word (r / 4) of the step, or Philox word k = t (R + 1) + r (p2pmg_device.h, oracle/philox.py)
+__device__ __forceinline__ int late_code(const EpisodeParams& p, const uint32_t* codes_a, size_t step_off, int t,
+                                         int r, int a, bool active) {
+  if (p.mode != 0 || !active) return 255;
+  if (p.rng == 1)
+    return (int)philox_round_code(t, p.R + 1, r, (uint32_t)p.episode, p.agent_offset + (uint32_t)a, p.eps_thr,
+                                  p.eps_all, p.seed_lo, p.seed_hi);
+  return (int)((codes_a[step_off + (size_t)(r >> 2) * p.A] >> (8 * (r & 3))) & 0xFFu);
+}
+// workgroup shape of the general kernel: one wave, or (shared table) kSqWaves waves around one LDS
+// delta hash; the 64-agent tiles (33 KB per wave) take two
+template <int NC, bool WIDE, bool SQ>
+constexpr int general_wpb() {
+  return SQ ? ((WIDE && NC > 32) ? 2 : kSqWaves) : 1;
+}
+
+// episode_kernel<NC, WIDE, QT, B20, SQ>: WIDE = false: N = NC agents per scenario compiled in
+// (PRegs); WIDE = true: n = p.N <= NC agents (PTile), the community sizes 9..15 and 17..64.  Both
+// sum over j = 0..n-1 in order from +0.0 and divide by n as IEEE quotients, so a scenario gives the
+// same bits either way (tests/test_gpu_parity.py runs the tile form at the register form's sizes).
+template <int NC, bool WIDE, typename QT, bool B20, bool SQ>
+__global__ __launch_bounds__((kWave * general_wpb<NC, WIDE, SQ>())) void episode_kernel(const EpisodeParams p) {
+  constexpr int G = pow2ceil(NC);
   constexpr int SPW = kWave / G;
-  constexpr int WPB = SQ ? kSqWaves : 1;  // waves per workgroup
-  constexpr int PW = G > 8 ? SPW * N * N : 1;
-  constexpr int RW = G > 8 ? SPW * N : 1;
+  constexpr int WPB = general_wpb<NC, WIDE, SQ>();  // waves per workgroup
+  constexpr int PW = WIDE ? SPW * 2 * PTile<NC>::kTile : (G > 8 ? SPW * NC * NC : 1);
+  constexpr int RW = (WIDE || G > 8) ? SPW * NC : 1;
   __shared__ float shPall[WPB * PW];
   __shared__ float shRall[WPB * RW];
   __shared__ uint32_t hkey[SQ ? kSqSlots : 1];
@@ -486,14 +558,21 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
 
   const int wv = SQ ? (int)(threadIdx.x / kWave) : 0;
   const int lane = SQ ? (int)(threadIdx.x % kWave) : (int)threadIdx.x;
-  float* const shP = shPall + wv * PW;  // this wave's exchange tile
+  float* const shP = shPall + wv * PW;  // this wave's exchange tiles
   float* const shR = shRall + wv * RW;
   const int sl = lane / G;
   const int i = lane % G;
+  const int n = WIDE ? p.N : NC;  // agents per scenario
+  const float nf = (float)n;
+  // x / n (mean over the community, the even split): div_n's power-of-two multiply is the IEEE quotient
+  auto divn = [&](float x) -> float {
+    if constexpr (WIDE) return x / nf;
+    else return div_n<NC>(x);
+  };
   const int s = (blockIdx.x * WPB + wv) * SPW + sl;
-  const bool in_group = i < N;
+  const bool in_group = i < n;
   const bool active = in_group && (s < p.S);
-  const int a = active ? s * N + i : 0;
+  const int a = active ? s * n + i : 0;
   const int s_env = p.n_env == 1 ? 0 : (s < p.S ? s : 0);
   const int T = p.T;
   const int R1 = p.R + 1;
@@ -504,6 +583,17 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
   const size_t A = (size_t)p.A;
   const KC k = pin_constants(p);  // loop constants in VGPRs (no SGPR spill reloads on the chain)
   const Dims<B20> D{k.nt, k.nT, k.nb, k.np};
+  std::conditional_t<WIDE, PTile<NC>, PRegs<NC>> P;
+  if constexpr (WIDE) {
+    P.base = shP + sl * 2 * PTile<NC>::kTile;
+    P.i = i;
+    P.rd = 0;
+    P.wr = 0;
+  } else {
+    P.sh = shP;
+    P.i = i;
+    P.sl = sl;
+  }
 
   const uint32_t n_states = (uint32_t)(p.nt * p.nT * p.nb * p.np);
   constexpr bool shared = SQ;
@@ -525,7 +615,7 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
   float tin = active ? p.t_in[a] : k.setpoint;
   float tm = active ? p.t_m[a] : k.setpoint;
   // round 0 and the next state both have p2p = mean(-0 ... -0) / max_in = 0 (agent.py:203, community.py:161)
-  const int ip_zero = idx_plain(div_n<N>(0.0f) / mi, D.p());
+  const int ip_zero = idx_plain(divn(0.0f) / mi, D.p());
 
   // running offsets (no 64-bit multiplies in the loop)
   const float* envb = p.env + (size_t)s_env * kEnvStride;
@@ -580,10 +670,7 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
 #endif
     const CodeWords cw1r = step_codes(p, codes_a, c1o, t + 1 == T ? 0 : t + 1, a, W);
 
-    float row[N];
-    float col[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) { row[j] = 0.0f; col[j] = 0.0f; }
+    P.clear();
     int act = 0, ip = ip_zero;
     float hp = 0.0f;
     double soc_r = soc;  // tentative SoC of the current round
@@ -592,14 +679,14 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
     Row4<QT> rowR = row0;  // Q row of the final round's state (TD target Q[s, a])
 
     for (int r = 0; r < R1; ++r) {
-      const int code = (int)((cw >> (8 * r)) & 0xFF);
+      const int code = r < 8 ? (int)((cw >> (8 * r)) & 0xFF) : late_code(p, codes_a, tA * W, t, r, a, active);
       if (r > 0) {
-        exchange<N>(row, col, i, sl, shP);  // Jacobi: read the previous round's column (community.py:84-86)
+        P.next_round();  // Jacobi: read the previous round's column (community.py:84-86)
         // powers = -P[:, i] with the diagonal zeroed (community.py:76,81); p2p = mean / max_in (agent.py:203)
         float acc = 0.0f;
 #pragma unroll
-        for (int j = 0; j < N; ++j) acc = acc + (-((j == i) ? 0.0f : col[j]));
-        ip = idx_plain(FDIV(div_n<N>(acc), mi), D.p());
+        for (int j = 0; j < n; ++j) acc = acc + (-((j == i) ? 0.0f : P.colv(j)));
+        ip = idx_plain(FDIV(divn(acc), mi), D.p());
         // the final round's row is needed for the TD update even when exploring
         const bool need = code == 255 || (train && r == R1 - 1);
         rowR = gather_row(q + (need ? st.strip + (uint32_t)ip : a0) * kQPad);
@@ -615,23 +702,24 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
         out = (float)battery_rule((double)out, soc_r, bcap, p.bat_min, p.bat_max, p.bat_sqrt_eff);
       }
       const float so = sgn(out);
-      float f[N];
+      // filtered_j: powers_j where its sign differs from out's (agent.py:187-189)
+      auto filt = [&](int j) -> float {
+        const float pw = -((j == i || r == 0) ? 0.0f : P.colv(j));
+        return (so != sgn(pw)) ? pw : 0.0f;
+      };
       float tot = 0.0f;
 #pragma unroll
-      for (int j = 0; j < N; ++j) {
-        const float pw = -((j == i || r == 0) ? 0.0f : col[j]);
-        f[j] = (so != sgn(pw)) ? pw : 0.0f;
-        tot = tot + f[j];
-      }
+      for (int j = 0; j < n; ++j) tot = tot + filt(j);
       tot = fabsf(tot);
       if (tot == 0.0f) {
-        const float ev = div_n<N>(out * 1.0f);
+        const float ev = divn(out * 1.0f);
 #pragma unroll
-        for (int j = 0; j < N; ++j) row[j] = ev;
+        for (int j = 0; j < n; ++j) P.put(j, ev);
       } else {
         // |f_ii| = 0 (own power is -0): (out * 0) / tot == out * 0 exactly for any non-NaN tot
 #pragma unroll
-        for (int j = 0; j < N; ++j) row[j] = (j == i) ? (tot == tot ? out * 0.0f : tot) : FDIV(nabs_out(out) * f[j], tot);
+        for (int j = 0; j < n; ++j)
+          P.put(j, (j == i) ? (tot == tot ? out * 0.0f : tot) : FDIV(nabs_out(out) * filt(j), tot));
       }
       if (active && (rec & 96u)) {
         const size_t kk = (tA * R1) + (size_t)r * A;
@@ -655,11 +743,11 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
     pat.row = 0xFFFFFFFFu;
 
     // CommunityMicrogrid._assign_powers community.py:45-54 on the final P (diagonal kept)
-    exchange<N>(row, col, i, sl, shP);
+    P.next_round();
     float g = 0.0f, pp = 0.0f;
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const float pij = row[j], pji = col[j];
+    for (int j = 0; j < n; ++j) {
+      const float pij = P.rowv(j), pji = P.colv(j);
       const float ex = pair_exchange(pij, pji);
       g = g + (pij - ex);
       pp = pp + ex;
@@ -701,8 +789,10 @@ __global__ __launch_bounds__(SQ ? kWave * kSqWaves : kWave) void episode_kernel(
       if (rec & 16u) rec_tin[tA] = tin;
     }
     // avg_reward = sum_t mean_i r (community.py:179), canonical sequential order
-    const float m = group_sum<N>(rw, lane, i, sl, shR);
-    ep_sum = ep_sum + div_n<N>(m);
+    float m;
+    if constexpr (WIDE) m = group_sum_n<NC>(rw, i, sl, n, shR);
+    else m = group_sum<NC>(rw, lane, i, sl, shR);
+    ep_sum = ep_sum + divn(m);
     if constexpr (SQ) {
       if (train && (t % kSqFlushSteps == kSqFlushSteps - 1 || t + 1 == T)) lds_hash_flush(hkey, hval, dbase, WPB * kWave);
     }
@@ -785,8 +875,12 @@ __global__ void philox_codes_kernel(const EpisodeParams p, uint32_t* __restrict_
   if (k >= (size_t)p.T * p.A) return;
   const int t = (int)(k / p.A), a = (int)(k % p.A);
   const int R1 = p.R + 1, W = (R1 + 3) >> 2;
-  const uint64_t codes = philox_codes_of(p, t, p.agent_offset + (uint32_t)a);
-  for (int w = 0; w < W; ++w) words[((size_t)t * W + w) * p.A + a] = (uint32_t)(codes >> (32 * w));
+  const uint32_t gid = p.agent_offset + (uint32_t)a;
+  const uint64_t codes = philox_codes_of(p, t, gid);
+  for (int w = 0; w < W; ++w)
+    words[((size_t)t * W + w) * p.A + a] =
+        w < 2 ? (uint32_t)(codes >> (32 * w))
+              : philox_code_word(t, R1, w, (uint32_t)p.episode, gid, p.eps_thr, p.eps_all, p.seed_lo, p.seed_hi);
 }
 #endif
 
@@ -934,9 +1028,13 @@ __device__ __forceinline__ void prepass_one(const EpisodeParams& p, const PrepOu
     q.eps_thr = chain ? o.ep_thr[ep] : o.eps_thr;
     q.eps_all = chain ? (int)((o.ep_all >> ep) & 1u) : o.eps_all;
     const int R1 = p.R + 1, W = (R1 + 3) >> 2;
-    const uint64_t codes = philox_codes_of(q, t, p.agent_offset + (uint32_t)a);
+    const uint32_t gid = p.agent_offset + (uint32_t)a;
+    const uint64_t codes = philox_codes_of(q, t, gid);
     uint32_t* words = o.words + (size_t)ep * o.words_stride;
-    for (int w = 0; w < W; ++w) words[((size_t)t * W + w) * p.A + a] = (uint32_t)(codes >> (32 * w));
+    for (int w = 0; w < W; ++w)
+      words[((size_t)t * W + w) * p.A + a] =
+          w < 2 ? (uint32_t)(codes >> (32 * w))
+                : philox_code_word(t, R1, w, (uint32_t)q.episode, gid, q.eps_thr, q.eps_all, p.seed_lo, p.seed_hi);
   }
 }
 #if P2PMG_IN_PART(0)
@@ -2260,30 +2358,37 @@ void launch_rule_g(const EpisodeParams& p, float* hp_on, hipStream_t st) {
   hipLaunchKernelGGL(rule_episode_kernel<G>, dim3((p.S + SPW - 1) / SPW), dim3(kWave), 0, st, p, hp_on);
 }
 
-template <int N, typename QT, bool SQ>
+template <int NC, bool WIDE, typename QT, bool SQ>
 void launch_nq(const EpisodeParams& p, hipStream_t st) {
-  constexpr int SPW = kWave / pow2ceil(N);
-  constexpr int WPB = SQ ? kSqWaves : 1;
+  constexpr int SPW = kWave / pow2ceil(NC);
+  constexpr int WPB = general_wpb<NC, WIDE, SQ>();
   const int waves = (p.S + SPW - 1) / SPW;
   const int blocks = (waves + WPB - 1) / WPB;
   if (p.nt == 20 && p.nT == 20 && p.nb == 20 && p.np == 20)
-    hipLaunchKernelGGL((episode_kernel<N, QT, true, SQ>), dim3(blocks), dim3(kWave * WPB), 0, st, p);
+    hipLaunchKernelGGL((episode_kernel<NC, WIDE, QT, true, SQ>), dim3(blocks), dim3(kWave * WPB), 0, st, p);
   else
-    hipLaunchKernelGGL((episode_kernel<N, QT, false, SQ>), dim3(blocks), dim3(kWave * WPB), 0, st, p);
+    hipLaunchKernelGGL((episode_kernel<NC, WIDE, QT, false, SQ>), dim3(blocks), dim3(kWave * WPB), 0, st, p);
 }
 
-template <int N, typename QT>
+template <int NC, bool WIDE, typename QT>
 hipError_t launch_n(const EpisodeParams& p, hipStream_t st) {
   if (p.shared_q)
-    launch_nq<N, QT, true>(p, st);
+    launch_nq<NC, WIDE, QT, true>(p, st);
   else
-    launch_nq<N, QT, false>(p, st);
+    launch_nq<NC, WIDE, QT, false>(p, st);
   return hipGetLastError();
 }
 
+// N compiled in (registers): N in {1..8, 16}
 template <int N>
 hipError_t launch_nd(const EpisodeParams& p, int q_dtype, hipStream_t st) {
-  return q_dtype == 0 ? launch_n<N, double>(p, st) : launch_n<N, float>(p, st);
+  return q_dtype == 0 ? launch_n<N, false, double>(p, st) : launch_n<N, false, float>(p, st);
+}
+// any N <= NC at run time (LDS tiles)
+template <int NC>
+hipError_t launch_wide(const EpisodeParams& p, int q_dtype, hipStream_t st) {
+  if (p.N < 1 || p.N > NC) return hipErrorInvalidValue;
+  return q_dtype == 0 ? launch_n<NC, true, double>(p, st) : launch_n<NC, true, float>(p, st);
 }
 
 // ----------------------------------------------------------------- small kernels
@@ -2630,11 +2735,29 @@ hipError_t launch_general_part8(const EpisodeParams& p, int q_dtype, hipStream_t
   return p.N == 16 ? launch_nd<16>(p, q_dtype, stream) : hipErrorInvalidValue;
 }
 #endif
+#if P2PMG_IN_PART(9)
+hipError_t launch_tile_part9(const EpisodeParams& p, int q_dtype, int nc, hipStream_t stream) {
+  return nc == 16 ? launch_wide<16>(p, q_dtype, stream) : hipErrorInvalidValue;
+}
+#endif
+#if P2PMG_IN_PART(10)
+hipError_t launch_tile_part10(const EpisodeParams& p, int q_dtype, int nc, hipStream_t stream) {
+  return nc == 32 ? launch_wide<32>(p, q_dtype, stream) : nc == 64 ? launch_wide<64>(p, q_dtype, stream)
+                                                                   : hipErrorInvalidValue;
+}
+#endif
 #if P2PMG_IN_PART(0)
-hipError_t launch_episode(const EpisodeParams& p, int q_dtype, hipStream_t stream) {
-  if (p.N >= 1 && p.N <= 4) return launch_general_part6(p, q_dtype, stream);
-  if (p.N >= 5 && p.N <= 8) return launch_general_part7(p, q_dtype, stream);
-  return launch_general_part8(p, q_dtype, stream);
+// the general kernel: registers for N in {1..8, 16}, LDS tiles for every other N <= 64 (and for any
+// N <= 64 when tile != 0, the cross-check of the two forms)
+hipError_t launch_episode(const EpisodeParams& p, int q_dtype, int tile, hipStream_t stream) {
+  if (p.N < 1 || p.N > kMaxAgents) return hipErrorInvalidValue;
+  if (!tile) {
+    if (p.N <= 4) return launch_general_part6(p, q_dtype, stream);
+    if (p.N <= 8) return launch_general_part7(p, q_dtype, stream);
+    if (p.N == 16) return launch_general_part8(p, q_dtype, stream);
+  }
+  const int nc = general_tile_cap(p.N);
+  return nc == 16 ? launch_tile_part9(p, q_dtype, nc, stream) : launch_tile_part10(p, q_dtype, nc, stream);
 }
 #endif
 

@@ -282,7 +282,8 @@ int p2pmg_create(const p2pmg_config* cfg, int device, p2pmg_ctx** out) {
   if (cfg->rounds + 1 > p2pmg::kMaxRounds1) return P2PMG_E_UNSUPPORTED;
   if (cfg->n_actions != 3) return P2PMG_E_UNSUPPORTED;
   const int N = cfg->n_agents;
-  if (!((N >= 1 && N <= 8) || N == 16)) return P2PMG_E_UNSUPPORTED;
+  // any community size a scenario's wave holds (get_community takes any n_agents, community.py:198-204)
+  if (N > p2pmg::kMaxAgents) return P2PMG_E_UNSUPPORTED;
   if (cfg->q_dtype != P2PMG_Q_F64 && cfg->q_dtype != P2PMG_Q_F32) return P2PMG_E_INVALID;
   p2pmg_ctx* c = new (std::nothrow) p2pmg_ctx();
   if (!c) return P2PMG_E_NOMEM;
@@ -679,7 +680,8 @@ static bool fast_applies(const p2pmg_ctx* c, const p2pmg_episode_args* args) {
              (1LL << 32) &&
          (long long)c->T * c->A < (1LL << 32) && host_div_range(g.minutes_per_hour) &&
          g.temp_margin == 1.0f &&  // heating.py:90 (the kernel skips the / margin)
-         !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_PHILOX_INKERNEL)) && !env_general;
+         !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_TILE_KERNEL | P2PMG_FLAG_PHILOX_INKERNEL)) &&
+         !env_general;
 }
 
 // a chained fast-path launch (p2pmg_run_episodes): n episodes at eps[0..n), the caller's guess of
@@ -722,7 +724,7 @@ static int run_episode_impl(p2pmg_ctx* c, const p2pmg_episode_args* args, const 
                     (long long)c->T * c->A < (1LL << 32) && (long long)c->T * c->n_env * p2pmg::kEnvStride < (1LL << 32) &&
                     host_div_range(g.temp_margin) && g.n_time_states == 20 && g.n_temp_states == 20 &&
                     g.n_balance_states == 20 && g.n_p2p_states == 20 &&
-                    !(args->flags & P2PMG_FLAG_GENERAL_KERNEL) && !env_general;
+                    !(args->flags & (P2PMG_FLAG_GENERAL_KERNEL | P2PMG_FLAG_TILE_KERNEL)) && !env_general;
   // the general kernel writes unpacked records; fast / sq16 write packed rows (rec_pack) that
   // p2pmg_get_record unpacks into one staging buffer, so those launches allocate no [T][A] arrays
   // per record (configs[3] at full size: 35 GB less)
@@ -855,18 +857,22 @@ static int run_episode_impl(p2pmg_ctx* c, const p2pmg_episode_args* args, const 
     spw = std::min(spw, full);
   }
   const bool reset = (args->flags & P2PMG_FLAG_RESET_T0) != 0;
+  // the general kernel's LDS-tile form: every N outside {1..8, 16}, or any N on request
+  const bool tile = !fast && !sq16 &&
+                    ((args->flags & P2PMG_FLAG_TILE_KERNEL) != 0 || !((c->N >= 1 && c->N <= 8) || c->N == 16));
   p.reset_t0 = (ext && reset) ? 1 : 0;
   p.reset_sigma = args->reset_sigma;
   hipError_t e = fast   ? p2pmg::launch_episode_fast(p, c->pre[ps], c->rec_pack, g.q_dtype, spw,
                                                     produce ? &next : nullptr, r0, r1, c->stream)
                  : sq16 ? p2pmg::launch_episode_sq16(p, g.q_dtype, r0, r1, c->stream)
-                        : p2pmg::launch_episode(p, g.q_dtype, c->stream);
+                        : p2pmg::launch_episode(p, g.q_dtype, tile, c->stream);
   if (e != hipSuccess) return fail(c, P2PMG_E_HIP, std::string("episode launch: ") + hipGetErrorString(e));
   c->rec_fast_mask = ext ? (args->record & 127) : 0;
   c->rec_last_mask = args->record;
   c->rec_narrow = (fast || sq16) ? p.rec_narrow : 0;
   c->last_kernel = std::string(fast ? "episode_fast_kernel<" : sq16 ? "episode_sq16_kernel<" : "episode_kernel<") +
-                   std::to_string(c->N) + "," + (g.q_dtype == 0 ? "f64" : "f32") + ",R1=" + std::to_string(c->R + 1) +
+                   std::to_string(c->N) + (tile ? ",tile" + std::to_string(p2pmg::general_tile_cap(c->N)) : "") + "," +
+                   (g.q_dtype == 0 ? "f64" : "f32") + ",R1=" + std::to_string(c->R + 1) +
                    (ext ? (train ? ",train" : ",greedy") : "") + (g.shared_q ? ",shared" : "") +
                    (c->battery ? (ext && !p.bat_safe ? ",battery,range-checked>" : ",battery>") : ">");
   if (!ext && stamp) HIP_TRY(c, hipEventRecord(r1, c->stream));

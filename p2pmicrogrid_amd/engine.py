@@ -237,7 +237,8 @@ class DeviceCommunityBatch:
                     next_epsilon: Optional[float] = None):
         """Launch one episode for all scenarios (asynchronous; stream-ordered).
         philox: 'auto' | 'prepass' | 'inkernel' placement of the Philox draws.
-        kernel: 'auto' (the fast per-agent-table kernel whenever it applies) | 'general'.
+        kernel: 'auto' (the fast per-agent-table kernel whenever it applies) | 'general' | 'tile'
+            (the general kernel's LDS-tile form, which every N outside {1..8, 16} runs, at any N).
         scen_per_wave: fast kernel only, scenarios per 64-lane wave (0 = full waves).
         reset_sigma: end the episode with agent.reset() (community.py:181), i.e. exactly
         reset_temperatures_philox(episode + 1, reset_sigma), fused into the episode launch.
@@ -248,7 +249,7 @@ class DeviceCommunityBatch:
         for r in record:
             mask |= _lib.REC[r]
         flags = {"auto": 0, "prepass": _lib.FLAG_PHILOX_PREPASS, "inkernel": _lib.FLAG_PHILOX_INKERNEL}[philox]
-        flags |= {"auto": 0, "general": _lib.FLAG_GENERAL_KERNEL}[kernel]
+        flags |= {"auto": 0, "general": _lib.FLAG_GENERAL_KERNEL, "tile": _lib.FLAG_TILE_KERNEL}[kernel]
         if reset_sigma is not None:
             flags |= _lib.FLAG_RESET_T0
         if next_epsilon is not None:  # a guess of 0.0 is a real guess (P2PMG_FLAG_NEXT_EPSILON)

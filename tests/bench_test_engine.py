@@ -62,7 +62,7 @@ class BenchOracleEngine(OracleEngine):
 
 
 class BenchOracleDQNEngine:
-    """The DeviceDQNBatch calls main_dqn makes, on oracle/dqn.py (one shared network)."""
+    """The DeviceDQNBatch calls run_dqn makes, on oracle/dqn.py (one shared network)."""
 
     def __init__(self, S, N, R, T, shared=True, device=0, scenario_offset=0, init_seed=0, seed=42, grad_segments=1,
                  agents_per_block=0):

@@ -62,6 +62,10 @@ class OracleEngine:
     def episode_rewards(self):
         return np.stack(self._chain)
 
+    def set_hp_levels(self, levels):
+        ob = self._ensure()
+        ob.hp_levels = np.asarray(levels, np.float32).reshape(self.S, self.N, 3).copy()
+
     def set_battery(self, capacity, min_soc=0.1, max_soc=0.9, efficiency=0.9, soc0=0.5):
         ob = self._ensure()
         ob.battery_capacity = np.broadcast_to(np.asarray(capacity, np.float64), (self.S, self.N)).copy()

@@ -10,7 +10,7 @@ import torch.multiprocessing as mp
 from p2pmicrogrid_amd.distributed import ShardedTrainer, shard
 
 S_TOTAL, N, R, T, EPISODES = 9, 2, 1, 24, 3
-PRIMARY_ONLY = ("--schedule-episodes", "0", "--secondary", "none")  # bench.py: configs[1] line only
+PRIMARY_ONLY = ("--schedule-episodes", "0", "--secondary", "none", "--extra", "")  # bench.py: configs[1] line only
 
 
 def _free_port():
@@ -337,14 +337,16 @@ def test_bench_host_rehearsal_dqn():
 
 SMALL_DEFAULT_LINE = ("--steps", "2", "--warmup", "1", "--horizon", "12", "--schedule-episodes", "24",
                       "--eps-windows", "6,15", "--eps-window-steps", "3", "--secondary-agents", "4",
-                      "--secondary-horizon", "12", "--secondary-steps", "2", "--secondary-warmup", "1")
+                      "--secondary-horizon", "12", "--secondary-steps", "2", "--secondary-warmup", "1",
+                      "--extra-horizon", "12", "--extra-steps", "2", "--extra-warmup", "1")
 
 
 def _default_line(world, scen_per_rank):
-    root, env = _bench_env()
+    root, env = _bench_env(P2PMG_BENCH_TEST_DQN_ENGINE="bench_test_engine:BenchOracleDQNEngine")
     extra = ("--gpus", str(world)) if world > 1 else ()
     return _bench_line(root, env, *extra, "--scenarios", str(scen_per_rank),
-                       "--secondary-scenarios", str(scen_per_rank), *SMALL_DEFAULT_LINE)
+                       "--secondary-scenarios", str(scen_per_rank), "--extra-scenarios", str(scen_per_rank),
+                       *SMALL_DEFAULT_LINE)
 
 
 @pytest.fixture(scope="module")
@@ -385,7 +387,21 @@ def test_bench_default_line_carries_configs2_secondary_and_value_at_eps(world, d
         assert len(d["launcher"]["rank_exit_codes"]) == world
         assert s["exchange"] == "host-rehearsal" and "exchange_fallback" in s  # no RCCL in the test engine
         assert len(s["rank_times_s"]) == world
+    # the further BASELINE configs on the same ranks: configs[4] (DQN, shared network, gradient-segment
+    # exchange at world > 1) and configs[3] (heterogeneous mixes, per-agent tables, battery)
+    q, y = d["secondary_dqn"], d["secondary_year"]
+    assert "error" not in q and "error" not in y, (q, y)
+    assert q["steps"] == 2 and q["value"] > 0 and q["roofline"]["bound"] == "mfma"
+    assert q["config"]["agent_steps_per_step"] == 8 * 2 * 12 and q["network_replicas_identical"]
+    assert q["grad_layout"] and "setup_s" in q
+    assert y["steps"] == 2 and y["value"] > 0 and y["config"]["battery"] and not y["config"]["shared_q"]
+    assert y["config"]["agent_steps_per_step"] == 8 * 4 * 12 and y["config"]["workload"].startswith("configs[3]")
+    assert y["setup_s"]["inputs"] >= 0
+    if world > 1:
+        assert q["exchange"] == "host-rehearsal" and "exchange_fallback" in q and len(q["rank_times_s"]) == world
     w1 = default_line_world1
+    assert q["mean_episode_reward"] == pytest.approx(w1["secondary_dqn"]["mean_episode_reward"], rel=1e-6)
+    assert y["mean_episode_reward"] == pytest.approx(w1["secondary_year"]["mean_episode_reward"], rel=1e-12)
     assert d["mean_episode_reward"] == pytest.approx(w1["mean_episode_reward"], rel=1e-12)
     assert ve["mean_episode_reward_last"] == pytest.approx(w1["value_at_eps"]["mean_episode_reward_last"], rel=1e-12)
     assert s["mean_episode_reward"] == pytest.approx(w1["secondary"]["mean_episode_reward"], rel=1e-12)

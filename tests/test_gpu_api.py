@@ -76,6 +76,47 @@ def test_object_api_reproduces_reference_driven_training(name):
         setup.homogeneous = False
 
 
+@pytest.mark.parametrize("n", [10, 24])
+def test_get_community_any_size_trains_like_oracle(n):
+    """get_community(QAgent, n, homogeneous=True) for community sizes outside {1..8, 16}
+    (community.py:198-204 replicates agent_dfs[0] n times): train_episode replays the reference's
+    np.random stream through the device (the general kernel's tile form) and equals the oracle fed
+    the community's own inputs and the same stream: rewards, decisions, episode reward, tables."""
+    from p2pmicrogrid_amd import community, setup
+    from p2pmicrogrid_amd.agent import QAgent
+    from p2pmicrogrid_amd.environment import env
+    from oracle.restatement import reference_replay_codes
+    setup.homogeneous = True  # HPHeating reads the module flag (heating.py:101,149)
+    try:
+        np.random.seed(42)
+        com = community.get_community(QAgent, n, homogeneous=True)
+        T, R = len(env), setup.rounds
+        time_f, t_out = env.arrays()
+        load = np.stack([a.load_series(T) for a in com.agents]).astype(np.float32)
+        pv = np.stack([a.pv.series(T) for a in com.agents]).astype(np.float32)
+        max_in = np.array([np.float32(a.max_in) for a in com.agents], np.float32)
+        ob = OracleBatch(S=1, N=n, R=R, load_w=load[None], pv_w=pv[None], max_in=max_in[None],
+                         env_time=np.asarray(time_f, np.float32)[None], env_tout=np.asarray(t_out, np.float32)[None])
+        rs = np.random.RandomState(42)  # homogeneous: nothing drawn before the first episode
+        for e in range(2):
+            ob.t_in = np.array([[a.heating.temperature[0] for a in com.agents]], np.float32)
+            ob.t_m = np.array([[a.heating.building_mass_temperature[0] for a in com.agents]], np.float32)
+            eps = com.agents[0].actor._epsilon
+            reward, loss = com.train_episode()
+            assert com._engine.last_kernel().startswith(f"episode_kernel<{n},tile"), com._engine.last_kernel()
+            out = ob.run_episode("train", codes=reference_replay_codes(rs, T, R, n, eps)[:, :, None, :], eps=eps)
+            assert loss == 0.0 and reward == float(out["episode_reward"][0]), e
+            assert np.array_equal(com.last_rewards, out["reward"][:, 0, :]), e
+            assert np.array_equal(com.decisions, np.array([0.0, 0.5, 1.0])[out["action"][:, :, 0, :]] * 3e3), e
+            tabs = np.stack([a.actor.q_table for a in com.agents])
+            assert np.array_equal(tabs.reshape(n, -1, 3), ob.q), e
+            assert np.count_nonzero(tabs) > 0
+        power, cost = com.run()  # greedy day with the learned tables
+        assert power.shape == (T, n) and np.all(np.isfinite(cost))
+    finally:
+        setup.homogeneous = False
+
+
 def test_standalone_qactor_matches_reference_sequence():
     """rl.QActor per-call API (select_action/train) on the device vs the reference's QActor."""
     from p2pmicrogrid_amd.rl import QActor

@@ -107,8 +107,9 @@ def _compare(out, rec, tag):
 CASES = [(2, 1, 96, "f64"), (3, 2, 48, "f64"), (5, 0, 40, "f64"), (8, 1, 24, "f64"), (16, 1, 12, "f64"),
          (1, 1, 30, "f64"), (2, 1, 96, "f32"), (4, 3, 20, "f32"), (2, 7, 10, "f64"), (6, 4, 10, "f32"),
          (7, 2, 16, "f64"), (3, 3, 12, "f32")]
-# kernel choice x scenarios per wave: the fast kernel (auto), partially filled fast waves, the general kernel
-KERNELS = [("auto", 0), ("auto", 5), ("general", 0)]
+# kernel choice x scenarios per wave: the fast kernel (auto), partially filled fast waves, the general
+# kernel, the general kernel's LDS-tile form (the form every N outside {1..8, 16} runs) at these sizes
+KERNELS = [("auto", 0), ("auto", 5), ("general", 0), ("tile", 0)]
 
 
 @pytest.mark.parametrize("kernel,spw", KERNELS)
@@ -135,6 +136,60 @@ def test_replay_batch_matches_oracle(N, R, T, q_dtype, kernel, spw):
     # greedy pass with the learned tables
     eng.run_episode("greedy", record=REC, kernel=kernel, scen_per_wave=spw)
     _compare(ob.run_episode("greedy"), eng.get_records(REC), "greedy")
+
+
+@pytest.mark.parametrize("q_dtype", ["f64", "f32"])
+@pytest.mark.parametrize("R", [0, 1, 2])
+@pytest.mark.parametrize("N", [9, 12, 15, 17, 24, 32, 64])
+def test_any_community_size_matches_oracle(N, R, q_dtype):
+    """Community sizes outside the compiled-in {1..8, 16} (get_community takes any n_agents,
+    community.py:198-204): the general kernel's LDS-tile form (P in two LDS tiles, sequential
+    j = 0..N-1 sums) against the oracle, replayed reference streams, 3 episodes + a greedy day."""
+    S, T = max(4, 256 // N), 12
+    inp = scenario_batch(S, N, T, seed=7)
+    ob = _oracle_for(inp, N, R, q_dtype)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = _device_for(inp, N, R, q_dtype)
+    rss = [np.random.RandomState(42 + s) for s in range(S)]
+    for e, eps in enumerate((0.81, 0.729, 0.2)):
+        codes = np.stack([reference_replay_codes(rs, T, R, N, eps) for rs in rss], axis=2)
+        eng.set_replay_codes(codes)
+        eng.run_episode("train", "replay", episode=e, epsilon=eps, record=REC)
+        assert eng.last_kernel().startswith(f"episode_kernel<{N},tile"), eng.last_kernel()
+        out = ob.run_episode("train", codes=codes, eps=eps)
+        _compare(out, eng.get_records(REC), (N, R, q_dtype, e))
+        assert np.array_equal(eng.episode_reward(), out["episode_reward"])
+        a, b = eng.get_temperatures()
+        assert np.array_equal(a, out["t_in_final"]) and np.array_equal(b, out["t_m_final"])
+    q = eng.get_q(dtype=np.float64 if q_dtype == "f64" else np.float32)
+    assert np.array_equal(q.reshape(S * N, -1, 3), ob.q)
+    eng.run_episode("greedy", record=REC)
+    _compare(ob.run_episode("greedy"), eng.get_records(REC), "greedy")
+    eng.close()
+
+
+@pytest.mark.parametrize("N,R,kernel,placement", [(3, 9, "general", "prepass"), (3, 9, "general", "inkernel"),
+                                                  (2, 8, "auto", "prepass"), (12, 11, "auto", "inkernel"),
+                                                  (5, 12, "tile", "prepass")])
+def test_more_than_eight_rounds_match_oracle(N, R, kernel, placement):
+    """R + 1 > 8 negotiation rounds (community.py:75 runs any `rounds`): rounds 8 and up take their
+    exploration codes one at a time (replay words 2.. and Philox words k = t (R + 1) + r), in the
+    register and tile forms, Philox pre-pass and in-kernel draws, against the oracle."""
+    S, T = 24, 10
+    inp = scenario_batch(S, N, T, seed=29)
+    ob = _oracle_for(inp, N, R)
+    ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
+    eng = _device_for(inp, N, R)
+    rss = [np.random.RandomState(42 + s) for s in range(S)]
+    for e, eps in enumerate((0.81, 0.5)):
+        eng.run_episode("train", "philox", episode=e, epsilon=eps, record=REC, philox=placement, kernel=kernel)
+        _compare(ob.run_episode("train", rng="philox", seed=42, episode=e, eps=eps), eng.get_records(REC), (N, R, e))
+    codes = np.stack([reference_replay_codes(rs, T, R, N, 0.6) for rs in rss], axis=2)
+    eng.set_replay_codes(codes)
+    eng.run_episode("train", "replay", episode=2, epsilon=0.6, record=REC, kernel=kernel)
+    _compare(ob.run_episode("train", codes=codes, eps=0.6), eng.get_records(REC), (N, R, "replay"))
+    assert np.array_equal(eng.get_q().reshape(S * N, -1, 3), ob.q)
+    eng.close()
 
 
 @pytest.mark.parametrize("placement", ["prepass", "inkernel"])
