@@ -206,7 +206,7 @@ __global__ __launch_bounds__((dqn_act_waves<NC, WIDE>() * kWave)) void dqn_act_k
     if constexpr (!WIDE) ru = load_unit(g.a);
   }
 
-  if (threadIdx.x < NC * NC) shP[0][threadIdx.x] = 0.0f;
+  for (int k2 = threadIdx.x; k2 < NC * NC; k2 += NW * kWave) shP[0][k2] = 0.0f;  // round 0 reads P = 0
   __syncthreads();
   int cur = 0;
   for (int r = 0; r < R1; ++r) {

@@ -144,10 +144,16 @@ __global__ __launch_bounds__(64) void chase2(const char* __restrict__ q, int lan
 // configs[1] with a one-step-ahead prefetch (stages=3 selects it; PF = 0 measures the same access
 // pattern without the prefetch): each step's 5 rows are one of 3 candidate sets, picked by a 2-bit
 // choice from the previous step's data (the final action: which of 3 next temperature bins).  With
-// PF, a step first touches every candidate set of the NEXT step (15 dword loads, results unused, issued
-// after this step's own rows so the in-order wait for those does not wait for them), so by the time the
-// choice is known the chosen rows are in L2 -- if the candidates can be known a step ahead, as the
-// next T_in / bins for each action are in episode_fast_kernel.
+// PF, one dword of every candidate row of step t + 1 (15 loads) is issued together with step t's own
+// rows, just before them, so by the time step t + 1's choice is known its rows are in L2 -- if the
+// candidates can be known a step ahead, as the next T_in / bins for each action are in
+// episode_fast_kernel.  The prefetched dwords are ordinary loads the compiler tracks, folded into the
+// result right after the step's rows are waited for (the in-order vmcnt has them complete then: they
+// are older).  Round 4's form was an inline-asm global_load_dword into a VGPR the compiler did not
+// know was in flight (it could reuse the register under the pending load: the fault of
+// profiles/r05_ab/helper_prefetch_ab.txt), and loads whose values are kept across a step make the
+// compiler copy (and so wait for) them, or wait for them before the step's rows (global_load_lds):
+// neither measured the schedule under study.  This one issues them in the same batch as the rows.
 template <bool PF>
 __global__ __launch_bounds__(64) void chase_pf(const char* __restrict__ q, int lanes, uint32_t pool, int steps,
                                                uint32_t* __restrict__ sink, unsigned long long* __restrict__ cyc) {
@@ -162,46 +168,45 @@ __global__ __launch_bounds__(64) void chase_pf(const char* __restrict__ q, int l
     return qwave + (qlane + pool_row(a, k) * kRowBytes);
   };
   uint32_t choice = mix(a) % 3u;
-  uint32_t acc = 0;
-  unsigned long long t0;
-  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  uint32_t acc = 0, pfacc = 0;
   uint4 lo[5];
   uint2 hi[5];
-#pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const char* p = row_of(0, choice, r);
-    lo[r] = *reinterpret_cast<const uint4*>(p);
-    hi[r] = *reinterpret_cast<const uint2*>(p + 16);
-  }
-  for (int t = 0; t < steps; ++t) {
-    if (PF && t + 1 < steps) {  // touch every candidate row of step t + 1
+  uint32_t pf[15];
+  // step t's batch: the prefetch of step t + 1's candidates (PF), then step t's chosen rows
+  auto issue = [&](int t) {
+    if (PF) {
+      const int tn = t + 1 < steps ? t + 1 : 0;
 #pragma unroll
       for (uint32_t c = 0; c < 3; ++c)
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {
-          uint32_t dummy;
-          asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(row_of(t + 1, c, r)) : "memory");
-        }
+        for (int r = 0; r < 5; ++r) pf[c * 5 + r] = *reinterpret_cast<const uint32_t*>(row_of(tn, c, r));
     }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const char* p = row_of(t, choice, r);
+      lo[r] = *reinterpret_cast<const uint4*>(p);
+      hi[r] = *reinterpret_cast<const uint2*>(p + 16);
+    }
+  };
+  unsigned long long t0;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  issue(0);
+  for (int t = 0; t < steps; ++t) {
     uint32_t x = (uint32_t)t;
 #pragma unroll
     for (int r = 0; r < 5; ++r) x ^= lo[r].x ^ lo[r].w ^ hi[r].y;
+    if (PF) {
+#pragma unroll
+      for (int k = 0; k < 15; ++k) pfacc ^= pf[k];
+    }
     const uint32_t h = mix(x);
     acc += h;
     choice = h % 3u;  // the final action picks the next step's candidate set
-    if (t + 1 < steps) {
-#pragma unroll
-      for (int r = 0; r < 5; ++r) {
-        const char* p = row_of(t + 1, choice, r);
-        lo[r] = *reinterpret_cast<const uint4*>(p);
-        hi[r] = *reinterpret_cast<const uint2*>(p + 16);
-      }
-    }
+    if (t + 1 < steps) issue(t + 1);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   unsigned long long t1;
   asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
-  sink[blockIdx.x * 64 + lane] = acc;
+  sink[blockIdx.x * 64 + lane] = acc + (pfacc & 1u);
   if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 

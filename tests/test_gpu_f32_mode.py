@@ -51,7 +51,7 @@ def test_f32_tables_track_reference_f64_trajectory(name):
         eng.run_episode("train", "replay", episode=e, epsilon=float(d["eps"][e]), record=REC)
         rec = eng.get_records(REC)
         act, idx = rec["action"][:, :, 0], unpack_index(rec["index"][:, :, 0])
-        same = np.all(act == d["train_action"][e], axis=1) & np.all(idx == d["train_idx"][e], axis=(1, 2))
+        same = np.all(act == d["train_action"][e], axis=(1, 2)) & np.all(idx == d["train_idx"][e], axis=(1, 2, 3))
         upto = len(same) if same.all() else int(np.argmin(same))
         for k in ("reward", "cost", "grid", "p2p", "t_in"):
             r = _rel(rec[k][:upto, 0], d[f"train_{k}"][e][:upto])
