@@ -693,9 +693,12 @@ def traffic_per_episode(traffic, chained: bool):
     if not traffic:
         return None
     if chained and "hbm_bytes_per_episode" in traffic:
-        return traffic["hbm_bytes_per_episode"]
+        return traffic.get("hbm_bytes_calibrated_per_episode", traffic["hbm_bytes_per_episode"])
     single = traffic.get("one_launch_per_episode")
-    return (single or traffic).get("hbm_bytes_per_launch")
+    if single:
+        return single.get("hbm_bytes_per_launch")
+    # round 6: counter factors measured per access pattern (scripts/recalibrate_traffic.py)
+    return traffic.get("hbm_bytes_calibrated_per_launch", traffic.get("hbm_bytes_per_launch"))
 
 
 REFERENCE_EPISODES = 1000  # setup.py:30 max_episodes: the reference's training run (community.py:272-298)
@@ -968,6 +971,8 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
             assert out["table_replicas_identical"], f"shared-table replicas differ across ranks: {hashes}"
         if traffic:
             out["roofline"]["traffic_source"] = traffic.get("source")
+            if "calibration" in traffic:  # round 6: per-pattern counter factors, not a uniform x2
+                out["roofline"]["traffic_calibration"] = traffic["calibration"]["source"]
         if not shared and q_dtype == "f64" and N <= 8:  # the fast kernel's sector-granular traffic model
             eps_mid = epsilon_at(warmup + steps // 2)
             sm = sector_model_per_agent_step(N, R, eps_mid, battery or hetero)

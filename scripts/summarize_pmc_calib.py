@@ -32,7 +32,7 @@ def main():
     out = {"round": RND, "probe": "scripts/pmc_calib.hip (scripts/gpu_calib.sh)",
            "unit": "counter bytes (rocprofv3 KB x 1024) per byte the pattern moves", "patterns": {}}
     for it in items:
-        k = it["launch"] - 1  # dispatches are 1-based, in launch order: fill, fill, then the patterns
+        k = it["launch"]  # 0-based position in launch order: fill, fill, then the patterns
         kf, f = fetch[k]
         kw, w = write[k]
         assert kf == kw, (kf, kw)

@@ -13,6 +13,9 @@
 //   and_vmask       v_and_b32 with a loop-invariant VGPR mask
 //   add_f32         v_add_f32 (baseline)
 //   med3_f32        v_med3_f32
+//   cnd_*_among_3_adds     one select (VCC e32 / SGPR-pair e64) per three independent v_add_f32
+//   cmp_vcc_then_cnd_e32   v_cmp_e32 into VCC then v_cndmask_b32_e32 on it (the compiler's usual pair)
+//   cmp_sgpr_then_cnd_e64  v_cmp_e64 into an SGPR pair then v_cndmask_b32_e64 on it
 // ubench_rate K = 22 wrote "vcc" as a clobber of every asm block while reading it: the compiler may
 // not keep a value in VCC across such blocks, so that number is checked here against the explicit
 // forms.  Prints one JSON line per variant.
@@ -77,9 +80,35 @@ __global__ __launch_bounds__(256) void sel(unsigned* out, unsigned a, unsigned b
     } else if constexpr (K == 9) {
       X4(asm volatile("v_med3_f32 %0, %0, %4, 0\n v_med3_f32 %1, %1, %4, 0\n v_med3_f32 %2, %2, %4, 0\n v_med3_f32 %3, %3, %4, 0"
                       : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3) : "v"(fb));)
+    } else if constexpr (K == 10) {  // one VCC select among three independent adds
+      X4(asm volatile("v_cndmask_b32_e32 %0, %0, %8, vcc\n v_add_f32 %4, %4, %9\n v_add_f32 %5, %5, %9\n v_add_f32 %6, %6, %9\n"
+                      " v_cndmask_b32_e32 %1, %1, %8, vcc\n v_add_f32 %7, %7, %9\n v_add_f32 %4, %4, %9\n v_add_f32 %5, %5, %9\n"
+                      " v_cndmask_b32_e32 %2, %2, %8, vcc\n v_add_f32 %6, %6, %9\n v_add_f32 %7, %7, %9\n v_add_f32 %4, %4, %9\n"
+                      " v_cndmask_b32_e32 %3, %3, %8, vcc\n v_add_f32 %5, %5, %9\n v_add_f32 %6, %6, %9\n v_add_f32 %7, %7, %9"
+                      : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3) : "v"(b), "v"(fb));)
+    } else if constexpr (K == 11) {  // one SGPR-pair select among three independent adds
+      X4(asm volatile("v_cndmask_b32_e64 %0, %0, %8, %10\n v_add_f32 %4, %4, %9\n v_add_f32 %5, %5, %9\n v_add_f32 %6, %6, %9\n"
+                      " v_cndmask_b32_e64 %1, %1, %8, %10\n v_add_f32 %7, %7, %9\n v_add_f32 %4, %4, %9\n v_add_f32 %5, %5, %9\n"
+                      " v_cndmask_b32_e64 %2, %2, %8, %10\n v_add_f32 %6, %6, %9\n v_add_f32 %7, %7, %9\n v_add_f32 %4, %4, %9\n"
+                      " v_cndmask_b32_e64 %3, %3, %8, %10\n v_add_f32 %5, %5, %9\n v_add_f32 %6, %6, %9\n v_add_f32 %7, %7, %9"
+                      : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3) : "v"(b), "v"(fb), "s"(sm));)
+    } else if constexpr (K == 12) {  // the compiler's pair: v_cmp into VCC, v_cndmask_e32 on it
+      X4(asm volatile("v_cmp_gt_f32_e32 vcc, %4, %5\n v_cndmask_b32_e32 %0, %0, %6, vcc\n"
+                      " v_cmp_gt_f32_e32 vcc, %5, %4\n v_cndmask_b32_e32 %1, %1, %6, vcc\n"
+                      " v_cmp_gt_f32_e32 vcc, %4, %5\n v_cndmask_b32_e32 %2, %2, %6, vcc\n"
+                      " v_cmp_gt_f32_e32 vcc, %5, %4\n v_cndmask_b32_e32 %3, %3, %6, vcc"
+                      : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3) : "v"(f0), "v"(fb), "v"(b) : "vcc");)
+    } else if constexpr (K == 13) {  // the same with the compare into an SGPR pair
+      uint64_t t0, t1;
+      X4(asm volatile("v_cmp_gt_f32_e64 %4, %6, %7\n v_cndmask_b32_e64 %0, %0, %8, %4\n"
+                      " v_cmp_gt_f32_e64 %5, %7, %6\n v_cndmask_b32_e64 %1, %1, %8, %5\n"
+                      " v_cmp_gt_f32_e64 %4, %6, %7\n v_cndmask_b32_e64 %2, %2, %8, %4\n"
+                      " v_cmp_gt_f32_e64 %5, %7, %6\n v_cndmask_b32_e64 %3, %3, %8, %5"
+                      : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "=&s"(t0), "=&s"(t1) : "v"(f0), "v"(fb), "v"(b));)
     }
   }
-  out[blockIdx.x * blockDim.x + threadIdx.x] = x0 + x1 + x2 + x3 + (unsigned)(f0 + f1 + f2 + f3) + (unsigned)sm;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x0 + x1 + x2 + x3 + (unsigned)(f0 + f1 + f2 + f3) + (unsigned)sm +
+                                                (unsigned)vm;
 }
 
 int main() {
@@ -94,9 +123,11 @@ int main() {
   hipEventCreate(&e1);
   // VALU instructions per pattern instance (the SALU s_movs of K = 2, 3 are listed separately)
   const char* names[] = {"cnd_vcc_e32", "cnd_sgpr_e64", "cnd_smov_vcc", "cnd_smov_sgpr", "cnd_consumed",
-                         "add_consumed", "bfi_vmask", "and_vmask", "add_f32", "med3_f32"};
-  const double valu[] = {1, 1, 1, 1, 2, 2, 1, 1, 1, 1};
-  const double salu[] = {0, 0, 2, 1, 0, 0, 0, 0, 0, 0};
+                         "add_consumed", "bfi_vmask", "and_vmask", "add_f32", "med3_f32",
+                         "cnd_vcc_e32_among_3_adds", "cnd_sgpr_e64_among_3_adds", "cmp_vcc_then_cnd_e32",
+                         "cmp_sgpr_then_cnd_e64"};
+  const double valu[] = {1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 4, 4, 2, 2};
+  const double salu[] = {0, 0, 2, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   auto run = [&](auto k) {
     constexpr int K = decltype(k)::value;
     float best = 1e30f;
@@ -125,6 +156,10 @@ int main() {
   run(std::integral_constant<int, 7>{});
   run(std::integral_constant<int, 8>{});
   run(std::integral_constant<int, 9>{});
+  run(std::integral_constant<int, 10>{});
+  run(std::integral_constant<int, 11>{});
+  run(std::integral_constant<int, 12>{});
+  run(std::integral_constant<int, 13>{});
   hipFree(out);
   return 0;
 }

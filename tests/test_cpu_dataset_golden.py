@@ -58,3 +58,19 @@ def test_dataframe_to_dataset_matches_reference(reference_db):
     assert d.data.dtype == np.float32
     assert np.array_equal(d.data, reference_db["train_ds_x"])
     assert np.array_equal(d.rolled, reference_db["train_ds_rolled"])
+
+
+def test_shared_scenario_inputs_equal_serial_generation():
+    """bench.py generates configs[3]'s year of inputs with a worker pool into shared memory
+    (dataset.SharedScenarioInputs): the same arrays bit for bit as scenario_batch + apply_asset_mix,
+    for a shard that starts and ends inside generator blocks."""
+    from p2pmicrogrid_amd.dataset import SharedScenarioInputs, apply_asset_mix, asset_mix, scenario_batch
+    S, N, T, first = 300, 3, 200, 200
+    mix = asset_mix(S, N, first_scenario=first, battery_j=36e6)
+    ref = apply_asset_mix(scenario_batch(S, N, T, first_scenario=first), mix)
+    with SharedScenarioInputs(S, N, T, workers=2, first_scenario=first, mix=mix) as sh:
+        got = sh.inputs
+        for k in ("time", "t_out", "load_w", "pv_w", "max_in", "t_in0", "t_m0", "load_ratings", "pv_ratings"):
+            a, b = getattr(ref, k), getattr(got, k)
+            assert a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a, b), k
+        del got, a, b
