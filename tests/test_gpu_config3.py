@@ -66,6 +66,12 @@ def _cmp(out, rec, tag):
     (2, 1, 96, "f64", False, True, True),      # N = 2 with a battery: no round-1 candidate rows
     (3, 0, 24, "f32", False, True, True),
     (8, 1, 24, "f32", False, True, False),
+    # community sizes outside {1..8, 16}: the general kernel's LDS-tile form with the shared table's
+    # delta hash (4 waves per workgroup; 2 at 64-agent capacity) and the battery rule
+    (10, 1, 24, "f32", True, True, False),
+    (24, 2, 16, "f64", True, False, True),
+    (40, 1, 12, "f32", True, True, True),
+    (12, 1, 24, "f64", False, True, True),
 ])
 def test_shared_battery_hetero_match_oracle(N, R, T, q_dtype, shared, battery, hetero):
     S = 24
