@@ -391,7 +391,44 @@ __global__ __launch_bounds__((dqn_act_waves<NC, WIDE>() * kWave)) void dqn_act_k
   do {               \
   } while (0)
 #endif
-template <int N, int AGW>
+// The shared network's post-exchange Adam step of parameter k (NSEG >= d.n_segs): the gathered
+// segments summed in global segment order, the mean over every agent of every rank, clip, Keras Adam
+// (beta1 .9, beta2 .999) and Trainer._soft_update (rl.py:307-359).  Every segment's value and the Adam
+// state are loaded before the first add (one memory round trip).  Returns the new weight; `store`:
+// writes the new moments, weight and soft-updated target to the *_out arrays.  One function for the
+// standalone launch and the act kernel's fused form, so both give the same bits.
+template <int NSEG>
+__device__ __forceinline__ float adam_shared_param(const DqnParams& d, int k, bool store) {
+  const int n = d.n_segs;
+  float sv[NSEG];
+#pragma unroll
+  for (int g = 0; g < NSEG; ++g) sv[g] = g < n ? d.segs[(size_t)g * kNetStride + k] : 0.0f;
+  const float m0 = d.adam_m[k], v0 = d.adam_v[k], w0 = d.theta[k];
+  const float tg0 = store ? d.target[k] : 0.0f;
+  float t = sv[0];
+#pragma unroll
+  for (int g = 1; g < NSEG; ++g) t = g < n ? t + sv[g] : t;  // segs 0 + 1 + ... + n-1, in order
+  float gk = t * d.inv_agents;
+  if (k < kOffB1) gk = fminf(fmaxf(gk, -d.clip), d.clip);
+  const float m = m0 + (gk - m0) * d.b1c;
+  const float v = v0 + (gk * gk - v0) * d.b2c;
+  const float w = w0 - (m * d.lr_t) / (sqrtf(v) + d.adam_eps);
+  if (store) {
+    d.m_out[k] = m;
+    d.v_out[k] = v;
+    d.theta_out[k] = w;
+    d.target_out[k] = d.tau_c * tg0 + d.tau * w;
+  }
+  return w;
+}
+
+// ADAM: the previous env step's shared Adam step is still pending (the multi-segment / multi-rank
+// path): every workgroup computes the new value of each weight it reads from the gathered segments
+// (adam_shared_param, the same bits as dqn_adam_shared_kernel), and workgroup 0, whose threads cover
+// every parameter once, stores the new state into the other half of the runtime's double buffer, so
+// no workgroup of this launch reads a value another one wrote.  This replaces a 4,609-parameter launch
+// per env step (one launch plus a memory round trip) with loads issued among the act prologue's own.
+template <int N, int AGW, bool ADAM>
 __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) {
   static_assert(AGW == 8 || AGW == 16, "8 or 16 agent slots per workgroup");
   constexpr int SPW = AGW / N;          // scenarios per workgroup
@@ -455,21 +492,29 @@ __global__ __launch_bounds__(256) void dqn_act_shared_kernel(const DqnParams d) 
   // (vmcnt counts loads and stores in issue order)
   const int32_t n_added = (agent_thr && p.mode != 1) ? d.added[a] : 0;
   const float ep_prev = (tid < SPW && s0 + tid < p.S && t != 0) ? d.ep_acc[s0 + tid] : 0.0f;
+  // weight k as this launch uses it; ADAM: after the pending step, stored by workgroup 0's owner
+  // thread of k (layer 1: wave 0; W2: every thread; b2 / W3: lanes c16 = 0; b3: thread 0)
+  const bool blk0 = ADAM && blockIdx.x == 0;
+  auto wt = [&](int k, bool owner) -> float {
+    if constexpr (ADAM) return adam_shared_param<kActAdamSegs>(d, k, blk0 && owner);
+    else return th[k];
+  };
   // layer 1 (thread = hidden unit u of agent slots 4 * (tid / 64) .. + 3): W1 column and b1
   const int u = l;
-  const float w10 = th[kOffW1 + 0 * kH + u], w11 = th[kOffW1 + 1 * kH + u], w12 = th[kOffW1 + 2 * kH + u],
-              w13 = th[kOffW1 + 3 * kH + u], w14 = th[kOffW1 + 4 * kH + u], b1 = th[kOffB1 + u];
+  const float w10 = wt(kOffW1 + 0 * kH + u, w == 0), w11 = wt(kOffW1 + 1 * kH + u, w == 0),
+              w12 = wt(kOffW1 + 2 * kH + u, w == 0), w13 = wt(kOffW1 + 3 * kH + u, w == 0),
+              w14 = wt(kOffW1 + 4 * kH + u, w == 0), b1 = wt(kOffB1 + u, w == 0);
   // layer 2 / 3 (wave w, lane: A operand W2[4 kk + g4][16 w + c16]; accumulator units 16 w + 4 g4 + r)
   float w2[16];
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk) w2[kk] = th[kOffW2 + (4 * kk + g4) * kH + 16 * w + c16];
+  for (int kk = 0; kk < 16; ++kk) w2[kk] = wt(kOffW2 + (4 * kk + g4) * kH + 16 * w + c16, true);
   float b2[4], w3[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    b2[r] = th[kOffB2 + 16 * w + 4 * g4 + r];
-    w3[r] = th[kOffW3 + 16 * w + 4 * g4 + r];
+    b2[r] = wt(kOffB2 + 16 * w + 4 * g4 + r, c16 == 0);
+    w3[r] = wt(kOffW3 + 16 * w + 4 * g4 + r, c16 == 0);
   }
-  const float b3 = th[kOffB3];
+  const float b3 = wt(kOffB3, tid == 0);
   // every round's exploration draw (or replayed code) ahead of the rounds: they depend only on
   // (t, episode, agent), so they run under the prologue's load latency, off the rounds' chain
   uint64_t codes_pack = ~0ull;  // byte r: code of round r < 8 (255 = greedy); later rounds are drawn in the loop
@@ -1246,38 +1291,71 @@ __global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kerne
   d.target[k] = d.tau_c * tg0 + d.tau * w0;
 }
 
+// The segment fold alone (the multi-segment / multi-rank path): the same 16 runs, summed in the same
+// order as dqn_reduce_adam_kernel, with SPT runs per thread, i.e. 16 / SPT waves per 64 parameters
+// instead of 16.  A segment of few partials (8 segments of 64 at configs[4]: 4 per run) gives each
+// wave a few loads, and the launch's wave count, not its bytes, set its duration.  The zero padding
+// is exact, as in dqn_reduce_adam_kernel.
+constexpr int kFoldBatch = 8;
+template <int SPT>
+__global__ __launch_bounds__(kRedParams * kRedSlices / SPT) void dqn_fold_kernel(const DqnParams d) {
+  __shared__ float part[kRedSlices][kRedParams];
+  const int j = threadIdx.x % kRedParams, grp = threadIdx.x / kRedParams;
+  const int k = blockIdx.x * kRedParams + j;
+  const int n = d.bps, per = (n + kRedSlices - 1) / kRedSlices;
+  if (k < kDqnParams) {
+    const float* g = d.grad + (size_t)blockIdx.y * n * kNetStride + k;
+    float v[SPT][kFoldBatch];  // the first kFoldBatch partials of each of the thread's runs, in flight together
+#pragma unroll
+    for (int q = 0; q < SPT; ++q) {
+      const int b0 = (grp * SPT + q) * per, b1 = min(n, b0 + per);
+#pragma unroll
+      for (int u = 0; u < kFoldBatch; ++u) v[q][u] = b0 + u < b1 ? g[(size_t)(b0 + u) * kNetStride] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < SPT; ++q) {
+      const int sl = grp * SPT + q, b0 = sl * per, b1 = min(n, b0 + per);
+      float s = 0.0f;
+#pragma unroll
+      for (int u = 0; u < kFoldBatch; ++u) s += v[q][u];
+      for (int b = b0 + kFoldBatch; b < b1; ++b) s += g[(size_t)b * kNetStride];
+      part[sl][j] = s;
+    }
+  }
+  __syncthreads();
+  if (grp != 0 || k >= kDqnParams) return;
+  float t = part[0][j];
+#pragma unroll
+  for (int r = 1; r < kRedSlices; ++r) t += part[r][j];
+  d.segs[(size_t)(d.seg_first + blockIdx.y) * kNetStride + k] = t;
+}
+
 // shared network over several segments / ranks: the segments' sum in global segment order, the mean
 // over every agent of every rank, clip, Adam, soft update (every rank computes the same values)
 // Latency, not bandwidth (4609 parameters): the Adam state and every segment's value are loaded
 // before the first add (one memory round trip instead of one per segment), then summed in order.
+// The *_out arrays may be the inputs (in place: each thread reads and writes its own parameter only).
 constexpr int kAdamSegBatch = 16;
 __global__ __launch_bounds__(256) void dqn_adam_shared_kernel(const DqnParams d) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= kDqnParams) return;
-  const float m0 = d.adam_m[k], v0 = d.adam_v[k], w0 = d.theta[k], tg0 = d.target[k];
-  const int n = d.n_segs;
-  float t;
-  if (n <= kAdamSegBatch) {
-    float sv[kAdamSegBatch];
-#pragma unroll
-    for (int g = 0; g < kAdamSegBatch; ++g) sv[g] = g < n ? d.segs[(size_t)g * kNetStride + k] : 0.0f;
-    t = sv[0];
-#pragma unroll
-    for (int g = 1; g < kAdamSegBatch; ++g) t = g < n ? t + sv[g] : t;  // segs 0 + 1 + ... + n-1, in order
-  } else {
-    t = d.segs[k];
-    for (int g = 1; g < n; ++g) t += d.segs[(size_t)g * kNetStride + k];
+  if (d.n_segs <= kAdamSegBatch) {
+    (void)adam_shared_param<kAdamSegBatch>(d, k, true);
+    return;
   }
+  const float m0 = d.adam_m[k], v0 = d.adam_v[k], w0 = d.theta[k], tg0 = d.target[k];
+  float t = d.segs[k];
+  for (int g = 1; g < d.n_segs; ++g) t += d.segs[(size_t)g * kNetStride + k];
   float gk = t * d.inv_agents;
   if (k < kOffB1) gk = fminf(fmaxf(gk, -d.clip), d.clip);
-  // adam_update's arithmetic on the preloaded state (Keras Adam, then Trainer._soft_update rl.py:335-354)
+  // adam_shared_param's arithmetic
   const float m = m0 + (gk - m0) * d.b1c;
   const float v = v0 + (gk * gk - v0) * d.b2c;
   const float w = w0 - (m * d.lr_t) / (sqrtf(v) + d.adam_eps);
-  d.adam_m[k] = m;
-  d.adam_v[k] = v;
-  d.theta[k] = w;
-  d.target[k] = d.tau_c * tg0 + d.tau * w;
+  d.m_out[k] = m;
+  d.v_out[k] = v;
+  d.theta_out[k] = w;
+  d.target_out[k] = d.tau_c * tg0 + d.tau * w;
 }
 
 // QNetwork.call on explicit rows (object API, rl.py:147-148): one thread per row
@@ -1308,21 +1386,31 @@ __global__ void dqn_forward_kernel(const float* __restrict__ th, int n, const fl
 
 }  // namespace
 
-hipError_t launch_dqn_act(const DqnParams& d, hipStream_t st) {
+static bool act_shared_mfma(const DqnParams& d) {
   // sizes the MFMA act kernel is built for (its action records pack 8 rounds)
   const bool mfma_n = ((d.e.N >= 1 && d.e.N <= 8) || d.e.N == 16) && d.e.R + 1 <= 8;
-  if (d.n_nets == 1 && !d.act_wave && mfma_n) {  // one shared network: AGW agents per workgroup on MFMA tiles
+  return d.n_nets == 1 && !d.act_wave && mfma_n;
+}
+
+bool dqn_act_fuses_adam(const DqnParams& d) { return act_shared_mfma(d) && d.n_segs >= 1 && d.n_segs <= kActAdamSegs; }
+
+hipError_t launch_dqn_act(const DqnParams& d, hipStream_t st) {
+  if (d.adam_pending && !dqn_act_fuses_adam(d)) return hipErrorInvalidValue;
+  if (act_shared_mfma(d)) {  // one shared network: AGW agents per workgroup on MFMA tiles
     // AGW = 16 agent slots per workgroup (default), or 8 (d.act_agw, P2PMG_ACT_AGW=8: more, shorter
-    // workgroups; N <= 8 only) -- the same results bit for bit
+    // workgroups; N <= 8 only) -- the same results bit for bit.  A pending Adam step: AGW = 16.
     switch (d.e.N) {
 #define P2PMG_DQN_ACT_SHARED(NN)                                                                                     \
   case NN: {                                                                                                         \
-    if (NN <= 8 && d.act_agw == 8) {                                                                                 \
-      constexpr int agw = NN <= 8 ? 8 : 16, spw = agw / NN;                                                          \
-      hipLaunchKernelGGL((dqn_act_shared_kernel<NN, agw>), dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d);     \
+    constexpr int spw = 16 / NN;                                                                                     \
+    if (d.adam_pending) {                                                                                            \
+      hipLaunchKernelGGL((dqn_act_shared_kernel<NN, 16, true>), dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d); \
+    } else if (NN <= 8 && d.act_agw == 8) {                                                                          \
+      constexpr int agw = NN <= 8 ? 8 : 16, spw8 = agw / NN;                                                         \
+      hipLaunchKernelGGL((dqn_act_shared_kernel<NN, agw, false>), dim3((d.e.S + spw8 - 1) / spw8), dim3(256), 0, st, \
+                         d);                                                                                         \
     } else {                                                                                                         \
-      constexpr int spw = 16 / NN;                                                                                   \
-      hipLaunchKernelGGL((dqn_act_shared_kernel<NN, 16>), dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d);      \
+      hipLaunchKernelGGL((dqn_act_shared_kernel<NN, 16, false>), dim3((d.e.S + spw - 1) / spw), dim3(256), 0, st, d); \
     }                                                                                                                \
     break;                                                                                                           \
   }
@@ -1369,8 +1457,13 @@ hipError_t launch_dqn_sample(const DqnParams& d, hipStream_t st) {
 
 hipError_t launch_dqn_reduce_adam(const DqnParams& d, int segments, bool adam, hipStream_t st) {
   if (segments < 1 || d.bps < 1 || (adam && segments != 1)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dqn_reduce_adam_kernel, dim3((kDqnParams + kRedParams - 1) / kRedParams, segments),
-                     dim3(kRedParams * kRedSlices), 0, st, d, adam ? 1 : 0);
+  const dim3 grid((kDqnParams + kRedParams - 1) / kRedParams, segments);
+  if (adam || d.fold_spt == 1)
+    hipLaunchKernelGGL(dqn_reduce_adam_kernel, grid, dim3(kRedParams * kRedSlices), 0, st, d, adam ? 1 : 0);
+  else if (d.fold_spt == 16)
+    hipLaunchKernelGGL(dqn_fold_kernel<16>, grid, dim3(kRedParams), 0, st, d);
+  else
+    hipLaunchKernelGGL(dqn_fold_kernel<4>, grid, dim3(kRedParams * 4), 0, st, d);
   return hipGetLastError();
 }
 

@@ -119,6 +119,11 @@ struct DqnParams {
   const float* batch;        // explicit [32][kTrans] batch (p2pmg_dqn_train_batch) or null
   int net;                   // network of the explicit batch
   float* loss_out;           // explicit batch: [1]
+  // shared network over segments / ranks: where the post-exchange Adam step stores the new weights,
+  // target and moments (the inputs themselves, or the other half of the runtime's double buffer)
+  float *theta_out, *target_out, *m_out, *v_out;
+  int adam_pending;          // 1: this act launch first applies the previous env step's gathered Adam step
+  int fold_spt;              // segment fold: runs per thread (4 default; 1 = dqn_reduce_adam_kernel, 16)
 };
 hipError_t launch_dqn_act(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_sample(const DqnParams& p, hipStream_t stream);
@@ -129,6 +134,11 @@ int dqn_train_blocks_per_cu();  // train workgroups resident per CU (the build's
 hipError_t launch_dqn_reduce_adam(const DqnParams& p, int segments, bool adam, hipStream_t stream);
 // sum of the n_segs segments in global order, then mean, clip, Adam, soft update
 hipError_t launch_dqn_adam_shared(const DqnParams& p, hipStream_t stream);
+// segments the act kernel's fused Adam step sums (more take the standalone launch)
+constexpr int kActAdamSegs = 8;
+// true when launch_dqn_act(p) with p.adam_pending = 1 can apply the pending Adam step itself (the shared
+// network's MFMA act kernel, at most kActAdamSegs segments)
+bool dqn_act_fuses_adam(const DqnParams& p);
 hipError_t launch_dqn_forward(const float* theta, int n, const float* x, float* q, hipStream_t stream);
 
 struct RcParams {

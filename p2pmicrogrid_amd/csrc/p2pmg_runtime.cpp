@@ -113,6 +113,8 @@ struct p2pmg_ctx {
   float* d_m = nullptr;
   float* d_v = nullptr;
   float* d_grad = nullptr;    // shared network: [d_blocks][kNetStride] partials
+  float* d_alt = nullptr;     // shared network: the other half of the Adam double buffer, [4][kNetStride]
+                              // (online, target, m, v) for the act kernel's fused post-exchange Adam step
   float* d_segs = nullptr;    // [nranks * d_seg_local][kNetStride] gradient segments, global order
   size_t d_segs_cap = 0;      // floats at d_segs
   float* h_segs = nullptr;    // pinned host copy of d_segs (host exchange)
@@ -382,6 +384,7 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   dfree(c->d_target);
   dfree(c->d_m);
   dfree(c->d_v);
+  dfree(c->d_alt);
   dfree(c->d_lr);
   dfree(c->d_grad);
   dfree(c->d_segs);
@@ -1545,6 +1548,7 @@ int p2pmg_dqn_setup(p2pmg_ctx* c, const p2pmg_dqn_config* cfg) {
     c->d_bps = (c->d_seg_agents + c->d_apb - 1) / c->d_apb;
     c->d_blocks = G * c->d_bps;
     HIP_TRY(c, dmalloc(&c->d_grad, (size_t)c->d_blocks * NS));
+    HIP_TRY(c, dmalloc(&c->d_alt, 4 * NS));
   } else {
     c->d_apb = 1;
     c->d_blocks = c->A;
@@ -1708,7 +1712,25 @@ static p2pmg::DqnParams dqn_params(p2pmg_ctx* c, const EpisodeParams& e) {
   d.clip = (float)q.clip;
   d.inv_agents = 1.0f / (float)((double)c->A * c->nranks);
   d.apb = c->d_apb;
+  d.theta_out = d.theta;  // the Adam steps store in place unless the episode loop binds the double buffer
+  d.target_out = d.target;
+  d.m_out = d.adam_m;
+  d.v_out = d.adam_v;
+  d.adam_pending = 0;
+  d.fold_spt = 4;
   return d;
+}
+
+// the network state an Adam step reads (in) and writes (out): online, target, m, v
+static void dqn_bind(p2pmg::DqnParams& d, float* const in[4], float* const out[4]) {
+  d.theta = in[0];
+  d.target = in[1];
+  d.adam_m = in[2];
+  d.adam_v = in[3];
+  d.theta_out = out[0];
+  d.target_out = out[1];
+  d.m_out = out[2];
+  d.v_out = out[3];
 }
 
 // Keras Adam step size for iteration `step` (1-based), float64 -> float32 (oracle/dqn.py::adam_lr)
@@ -1791,7 +1813,9 @@ static int dqn_gather_segments(p2pmg_ctx* c) {
   return P2PMG_OK;
 }
 
-static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
+// defer (the shared network's split path, act kernel able to fuse it): the post-exchange Adam step is
+// left pending (d.adam_pending) for the next env step's act launch, or dqn_settle after the last step
+static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same, bool defer) {
   // one env step trains every network once (community.py:158-168); the Adam step counters advance
   // only once every launch of the step is enqueued (a failed exchange leaves weights and counters
   // at the previous step: the Adam launch that would change the weights was not issued)
@@ -1808,7 +1832,8 @@ static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same) {
         const int rc = dqn_gather_segments(c);
         if (rc != P2PMG_OK) return rc;
       }
-      HIP_TRY(c, p2pmg::launch_dqn_adam_shared(d, c->stream));
+      if (defer) d.adam_pending = 1;
+      else HIP_TRY(c, p2pmg::launch_dqn_adam_shared(d, c->stream));
     }
   } else {
     HIP_TRY(c, p2pmg::launch_dqn_train(d, c->A, false, c->stream));
@@ -1853,6 +1878,8 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     d.act_wave = (v && !strcmp(v, "wave")) ? 1 : 0;
     const char* g = getenv("P2PMG_ACT_AGW");  // 8: the 8-slot MFMA act workgroups (tests, A/B)
     d.act_agw = (g && atoi(g) == 8) ? 8 : 16;
+    const char* f = getenv("P2PMG_FOLD_SPT");  // segment fold runs per thread: 1, 4 (default) or 16 (A/B)
+    d.fold_spt = f ? (atoi(f) == 1 ? 1 : (atoi(f) == 16 ? 16 : 4)) : 4;
   }
   c->last_kernel = std::string(c->n_nets == 1 && !d.act_wave ? "dqn_act_shared_kernel<" : "dqn_act_kernel<") +
                    std::to_string(c->N) + ">";
@@ -1861,17 +1888,59 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     rc = dqn_upload_lr_table(c);
     if (rc != P2PMG_OK) return rc;
   }
+  // The shared network's split path (segments / ranks): env step t's post-exchange Adam step runs
+  // inside env step t + 1's act launch, which reads the state from one half of a double buffer and
+  // stores the stepped state into the other (every act workgroup needs the new weights; workgroup 0
+  // stores them); the episode's last step, or any early return, settles into the primary arrays.
+  // Opt-in (P2PMG_DQN_ADAM=act): measured on the MI355X the fused form costs the act launch far more
+  // than the standalone Adam launch it saves, so the default is that launch.
+  const char* adam_env = getenv("P2PMG_DQN_ADAM");
+  const bool defer = mode == P2PMG_MODE_TRAIN && c->n_nets == 1 && (c->nranks > 1 || c->d_seg_local > 1) &&
+                     c->d_alt && p2pmg::dqn_act_fuses_adam(d) && adam_env && !strcmp(adam_env, "act");
+  const size_t NS = p2pmg::kNetStride;
+  float* const prim[4] = {c->d_theta, c->d_target, c->d_m, c->d_v};
+  float* const alt[4] = {c->d_alt, c->d_alt + NS, c->d_alt + 2 * NS, c->d_alt + 3 * NS};
+  bool on_alt = false;  // the current state sits in the alt half
+  auto settle = [&]() -> int {
+    float* const* cur = on_alt ? alt : prim;
+    if (d.adam_pending) {  // the pending step, from the current half into the primary arrays
+      dqn_bind(d, cur, prim);
+      d.adam_pending = 0;
+      HIP_TRY(c, p2pmg::launch_dqn_adam_shared(d, c->stream));
+    } else if (on_alt) {
+      for (int k = 0; k < 4; ++k)
+        HIP_TRY(c, hipMemcpyAsync(prim[k], alt[k], NS * 4, hipMemcpyDeviceToDevice, c->stream));
+    }
+    on_alt = false;
+    dqn_bind(d, prim, prim);
+    return P2PMG_OK;
+  };
   const int slot = (int)(c->n_timed % p2pmg_ctx::kRing);
   HIP_TRY(c, hipEventRecord(c->ring[2 * slot], c->stream));
   for (int t = 0; t < c->T; ++t) {
     d.t = t;
     d.e.mode = mode;
-    HIP_TRY(c, p2pmg::launch_dqn_act(d, c->stream));
+    if (d.adam_pending) dqn_bind(d, on_alt ? alt : prim, on_alt ? prim : alt);
+    const hipError_t e = p2pmg::launch_dqn_act(d, c->stream);
+    if (e != hipSuccess) {
+      (void)settle();
+      return fail(c, P2PMG_E_HIP, std::string("dqn act launch: ") + hipGetErrorString(e));
+    }
+    if (d.adam_pending) {  // applied: the stepped state is the current one
+      on_alt = !on_alt;
+      d.adam_pending = 0;
+      dqn_bind(d, on_alt ? alt : prim, on_alt ? alt : prim);
+    }
     if (mode == P2PMG_MODE_TRAIN) {
-      rc = dqn_train_step(c, d, same);
-      if (rc != P2PMG_OK) return rc;
+      rc = dqn_train_step(c, d, same, defer);
+      if (rc != P2PMG_OK) {
+        (void)settle();
+        return rc;
+      }
     }
   }
+  rc = settle();
+  if (rc != P2PMG_OK) return rc;
   HIP_TRY(c, hipEventRecord(c->ring[2 * slot + 1], c->stream));
   c->timed = true;
   c->n_timed++;

@@ -183,11 +183,35 @@ def _compare_episode(eng, out, mode, eps):
                                                        # community sizes outside {1..8, 16} (the act
                                                        # kernel's 16-wave form) and R + 1 > 8 rounds
                                                        (2, 10, 1, False, 0, 1), (1, 20, 2, True, 4, 1),
-                                                       (1, 33, 0, False, 0, 1), (2, 3, 8, True, 2, 1)])
+                                                       (1, 33, 0, False, 0, 1), (2, 3, 8, True, 2, 1),
+                                                       # 8 segments (the act kernel's fused Adam step at
+                                                       # its limit) and 16 (the standalone Adam launch)
+                                                       (8, 2, 1, True, 2, 8), (16, 1, 1, True, 1, 16)])
 def test_episodes_match_oracle(S, N, R, shared, apb, segments):
     """Fill + two training episodes + a greedy day, bit for bit: records, replay rings, losses,
     weights, target and Adam state (shared network: blocks of apb agents, `segments` gradient
     segments on one context, summed in segment order)."""
+    _episodes_vs_oracle(S, N, R, shared, apb, segments)
+
+
+@pytest.mark.parametrize("form", ["launch", "act", "fold1", "fold16"])
+@pytest.mark.parametrize("S,N,R,apb,segments", [(4, 3, 2, 5, 2), (8, 2, 1, 3, 4), (8, 16, 1, 4, 8)])
+def test_split_path_forms_match_oracle(monkeypatch, form, S, N, R, apb, segments):
+    """The shared network's multi-segment path in each of its forms, bit for bit the oracle's step
+    order (rl.py:307-359): the segment fold with 4 runs per thread (default), 1 (the reduce kernel's
+    1024-thread form, P2PMG_FOLD_SPT=1) or 16; the post-exchange Adam step as its own launch per env
+    step (default) or inside env step t + 1's act launch (P2PMG_DQN_ADAM=act: double-buffered network
+    state, the episode's last step settled into the primary arrays)."""
+    monkeypatch.delenv("P2PMG_DQN_ADAM", raising=False)
+    monkeypatch.delenv("P2PMG_FOLD_SPT", raising=False)
+    if form == "act":
+        monkeypatch.setenv("P2PMG_DQN_ADAM", "act")
+    elif form.startswith("fold"):
+        monkeypatch.setenv("P2PMG_FOLD_SPT", form[4:])
+    _episodes_vs_oracle(S, N, R, True, apb, segments)
+
+
+def _episodes_vs_oracle(S, N, R, shared, apb, segments):
     # the oracle's per-agent Python loops bound the larger communities: T = 16 there, two fill episodes
     # (the 31 transitions training needs, rl.py:234-235) and one training episode
     big = N not in (1, 2, 3, 4, 5, 6, 7, 8, 16)
