@@ -1296,8 +1296,7 @@ __global__ __launch_bounds__(kRedParams * kRedSlices) void dqn_reduce_adam_kerne
 // instead of 16.  A segment of few partials (8 segments of 64 at configs[4]: 4 per run) gives each
 // wave a few loads, and the launch's wave count, not its bytes, set its duration.  The zero padding
 // is exact, as in dqn_reduce_adam_kernel.
-constexpr int kFoldBatch = 8;
-template <int SPT>
+template <int SPT, int BATCH>
 __global__ __launch_bounds__(kRedParams * kRedSlices / SPT) void dqn_fold_kernel(const DqnParams d) {
   __shared__ float part[kRedSlices][kRedParams];
   const int j = threadIdx.x % kRedParams, grp = threadIdx.x / kRedParams;
@@ -1305,20 +1304,20 @@ __global__ __launch_bounds__(kRedParams * kRedSlices / SPT) void dqn_fold_kernel
   const int n = d.bps, per = (n + kRedSlices - 1) / kRedSlices;
   if (k < kDqnParams) {
     const float* g = d.grad + (size_t)blockIdx.y * n * kNetStride + k;
-    float v[SPT][kFoldBatch];  // the first kFoldBatch partials of each of the thread's runs, in flight together
+    float v[SPT][BATCH];  // the first BATCH partials of each of the thread's runs, in flight together
 #pragma unroll
     for (int q = 0; q < SPT; ++q) {
       const int b0 = (grp * SPT + q) * per, b1 = min(n, b0 + per);
 #pragma unroll
-      for (int u = 0; u < kFoldBatch; ++u) v[q][u] = b0 + u < b1 ? g[(size_t)(b0 + u) * kNetStride] : 0.0f;
+      for (int u = 0; u < BATCH; ++u) v[q][u] = b0 + u < b1 ? g[(size_t)(b0 + u) * kNetStride] : 0.0f;
     }
 #pragma unroll
     for (int q = 0; q < SPT; ++q) {
       const int sl = grp * SPT + q, b0 = sl * per, b1 = min(n, b0 + per);
       float s = 0.0f;
 #pragma unroll
-      for (int u = 0; u < kFoldBatch; ++u) s += v[q][u];
-      for (int b = b0 + kFoldBatch; b < b1; ++b) s += g[(size_t)b * kNetStride];
+      for (int u = 0; u < BATCH; ++u) s += v[q][u];
+      for (int b = b0 + BATCH; b < b1; ++b) s += g[(size_t)b * kNetStride];
       part[sl][j] = s;
     }
   }
@@ -1458,17 +1457,29 @@ hipError_t launch_dqn_sample(const DqnParams& d, hipStream_t st) {
 hipError_t launch_dqn_reduce_adam(const DqnParams& d, int segments, bool adam, hipStream_t st) {
   if (segments < 1 || d.bps < 1 || (adam && segments != 1)) return hipErrorInvalidValue;
   const dim3 grid((kDqnParams + kRedParams - 1) / kRedParams, segments);
-  if (adam || d.fold_spt == 1)
+  // the fold: runs of per = ceil(bps / 16) partials, the first 4 or 8 of each run loaded together
+  const bool b4 = (d.bps + kRedSlices - 1) / kRedSlices <= 4;
+#define P2PMG_FOLD(SPT)                                                                                           \
+  if (b4) hipLaunchKernelGGL((dqn_fold_kernel<SPT, 4>), grid, dim3(kRedParams * kRedSlices / SPT), 0, st, d);   \
+  else hipLaunchKernelGGL((dqn_fold_kernel<SPT, 8>), grid, dim3(kRedParams * kRedSlices / SPT), 0, st, d);
+  if (adam || d.fold_spt == 1) {
     hipLaunchKernelGGL(dqn_reduce_adam_kernel, grid, dim3(kRedParams * kRedSlices), 0, st, d, adam ? 1 : 0);
-  else if (d.fold_spt == 16)
-    hipLaunchKernelGGL(dqn_fold_kernel<16>, grid, dim3(kRedParams), 0, st, d);
-  else
-    hipLaunchKernelGGL(dqn_fold_kernel<4>, grid, dim3(kRedParams * 4), 0, st, d);
+  } else if (d.fold_spt == 2) {
+    P2PMG_FOLD(2)
+  } else if (d.fold_spt == 8) {
+    P2PMG_FOLD(8)
+  } else if (d.fold_spt == 16) {
+    P2PMG_FOLD(16)
+  } else {
+    P2PMG_FOLD(4)
+  }
+#undef P2PMG_FOLD
   return hipGetLastError();
 }
 
 hipError_t launch_dqn_adam_shared(const DqnParams& d, hipStream_t st) {
-  hipLaunchKernelGGL(dqn_adam_shared_kernel, dim3((kDqnParams + 255) / 256), dim3(256), 0, st, d);
+  const int tpb = d.adam_tpb == 64 || d.adam_tpb == 128 ? d.adam_tpb : 256;
+  hipLaunchKernelGGL(dqn_adam_shared_kernel, dim3((kDqnParams + tpb - 1) / tpb), dim3(tpb), 0, st, d);
   return hipGetLastError();
 }
 

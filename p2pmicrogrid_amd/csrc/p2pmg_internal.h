@@ -123,7 +123,8 @@ struct DqnParams {
   // target and moments (the inputs themselves, or the other half of the runtime's double buffer)
   float *theta_out, *target_out, *m_out, *v_out;
   int adam_pending;          // 1: this act launch first applies the previous env step's gathered Adam step
-  int fold_spt;              // segment fold: runs per thread (4 default; 1 = dqn_reduce_adam_kernel, 16)
+  int adam_tpb;              // post-exchange Adam launch: threads per workgroup (256 default; 64, 128)
+  int fold_spt;              // segment fold: runs per thread (4 default; 1 = dqn_reduce_adam_kernel; 2, 8, 16)
 };
 hipError_t launch_dqn_act(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_sample(const DqnParams& p, hipStream_t stream);

@@ -4,20 +4,22 @@
 # lines and rocprofv3 kernel stats of each form:
 #   split        the default split path (fold with 4 runs per thread, standalone Adam launch)
 #   splitfold1   the fold on the reduce kernel's 1024-thread form (P2PMG_FOLD_SPT=1, rounds 4-5)
-#   splitfold16  the fold with 16 runs per thread (P2PMG_FOLD_SPT=16)
+#   splitfoldK   the fold with K = 2, 8 or 16 runs per thread (P2PMG_FOLD_SPT=K)
 #   splitact     the Adam step inside the next env step's act launch (P2PMG_DQN_ADAM=act)
+#   splitadamK   the standalone Adam launch with K = 64 or 128 threads per workgroup (P2PMG_ADAM_TPB=K)
 # Output under gpurun_out/<tag>/dqn_split/.
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
 O="$R/gpurun_out/${1:-r06}/dqn_split"; mkdir -p "$O"
 FORMS="${2:-fused split splitfold1 splitfold16 splitact}"
 setform() {
-  unset P2PMG_DQN_ADAM P2PMG_FOLD_SPT
+  unset P2PMG_DQN_ADAM P2PMG_FOLD_SPT P2PMG_ADAM_TPB
   A="--grad-segments 8 --rccl-world1"
   case $1 in
     fused) A="" ;;
     splitfold1) export P2PMG_FOLD_SPT=1 ;;
-    splitfold16) export P2PMG_FOLD_SPT=16 ;;
+    splitfold*) export P2PMG_FOLD_SPT=${1#splitfold} ;;
     splitact) export P2PMG_DQN_ADAM=act ;;
+    splitadam*) export P2PMG_ADAM_TPB=${1#splitadam} ;;
   esac
 }
 for V in $FORMS; do

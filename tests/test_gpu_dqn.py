@@ -194,21 +194,54 @@ def test_episodes_match_oracle(S, N, R, shared, apb, segments):
     _episodes_vs_oracle(S, N, R, shared, apb, segments)
 
 
-@pytest.mark.parametrize("form", ["launch", "act", "fold1", "fold16"])
-@pytest.mark.parametrize("S,N,R,apb,segments", [(4, 3, 2, 5, 2), (8, 2, 1, 3, 4), (8, 16, 1, 4, 8)])
+_SPLIT_CASES = [(4, 3, 2, 5, 2), (8, 2, 1, 3, 4), (8, 16, 1, 4, 8)]
+
+
+@pytest.mark.parametrize("form,S,N,R,apb,segments",
+                         [(f, *c) for f in ("launch", "act") for c in _SPLIT_CASES] +
+                         [(f, 8, 16, 1, 4, 8) for f in ("fold1", "fold2", "fold8", "fold16")] +
+                         [("fold2", 4, 3, 2, 5, 2), ("adam64", 8, 16, 1, 4, 8)])
 def test_split_path_forms_match_oracle(monkeypatch, form, S, N, R, apb, segments):
     """The shared network's multi-segment path in each of its forms, bit for bit the oracle's step
     order (rl.py:307-359): the segment fold with 4 runs per thread (default), 1 (the reduce kernel's
-    1024-thread form, P2PMG_FOLD_SPT=1) or 16; the post-exchange Adam step as its own launch per env
-    step (default) or inside env step t + 1's act launch (P2PMG_DQN_ADAM=act: double-buffered network
+    1024-thread form, P2PMG_FOLD_SPT=1), 2, 8 or 16; the post-exchange Adam step as its own launch per env
+    step (default; 64-thread workgroups with P2PMG_ADAM_TPB=64) or inside env step t + 1's act launch (P2PMG_DQN_ADAM=act: double-buffered network
     state, the episode's last step settled into the primary arrays)."""
     monkeypatch.delenv("P2PMG_DQN_ADAM", raising=False)
     monkeypatch.delenv("P2PMG_FOLD_SPT", raising=False)
+    monkeypatch.delenv("P2PMG_ADAM_TPB", raising=False)
     if form == "act":
         monkeypatch.setenv("P2PMG_DQN_ADAM", "act")
     elif form.startswith("fold"):
         monkeypatch.setenv("P2PMG_FOLD_SPT", form[4:])
+    elif form.startswith("adam"):
+        monkeypatch.setenv("P2PMG_ADAM_TPB", form[4:])
     _episodes_vs_oracle(S, N, R, True, apb, segments)
+
+
+@pytest.mark.parametrize("spt", ["4", "2", "8", "16"])
+def test_fold_forms_agree_on_long_runs(monkeypatch, spt):
+    """Segments of 130 one-agent train workgroups (runs of 9 partials: the fold's 8-load batch and
+    its remainder loop; the oracle's per-agent training is too slow at this size): every fold form
+    trains the same network bit for bit as the reduce kernel's form (P2PMG_FOLD_SPT=1), which
+    test_split_path_forms_match_oracle pins to the oracle."""
+    S, N, T = 130, 2, 16
+    nets = {}
+    for form in ("1", spt):
+        monkeypatch.setenv("P2PMG_FOLD_SPT", form)
+        inp = scenario_batch(S, N, T)
+        eng = DeviceDQNBatch(S, N, 1, T, shared=True, init_seed=5, agents_per_block=1, grad_segments=2)
+        eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+        eng.set_profiles(inp.load_w, inp.pv_w)
+        eng.set_max_in(inp.max_in)
+        eng.set_temperatures(inp.t_in0, inp.t_m0)
+        for ep, (mode, eps) in enumerate((("fill", 1.0), ("fill", 1.0), ("train", 0.9), ("train", 0.5))):
+            eng.run_episode(mode, "philox", episode=ep, epsilon=eps, record=("loss",) if mode == "train" else ())
+        nets[form] = [eng.get_weights(k) for k in ("online", "target", "adam_m", "adam_v")] + [eng.get_record("loss")]
+        eng.close()
+    for a, b, k in zip(nets["1"], nets[spt], ("online", "target", "adam_m", "adam_v", "loss")):
+        _eq(b, a, k)
+    assert not np.array_equal(nets["1"][0], nets["1"][1])
 
 
 def _episodes_vs_oracle(S, N, R, shared, apb, segments):
