@@ -696,7 +696,7 @@ def traffic_per_episode(traffic, chained: bool):
         return traffic.get("hbm_bytes_calibrated_per_episode", traffic["hbm_bytes_per_episode"])
     single = traffic.get("one_launch_per_episode")
     if single:
-        return single.get("hbm_bytes_per_launch")
+        return single.get("hbm_bytes_calibrated_per_launch", single.get("hbm_bytes_per_launch"))
     # round 6: counter factors measured per access pattern (scripts/recalibrate_traffic.py)
     return traffic.get("hbm_bytes_calibrated_per_launch", traffic.get("hbm_bytes_per_launch"))
 

@@ -71,6 +71,15 @@ def main():
             d["hbm_bytes_calibrated_per_episode"] = r1 + w1
             d["read_bytes_calibrated_per_episode"] = r1
             d["gather_read_bytes_calibrated_per_episode"] = g1
+        single = d.get("one_launch_per_episode")
+        if single:  # the one-launch-per-episode figure (rounds 1-5 stored FETCH x 2 there too)
+            raw1 = single.get("raw") or {"fetch_size_bytes_per_launch": single["read_bytes_per_launch"] / 2.0,
+                                         "write_size_bytes_per_launch": single["write_bytes_per_launch"]}
+            single["raw"] = raw1
+            r1, w1, g1 = calib(raw1["fetch_size_bytes_per_launch"], raw1["write_size_bytes_per_launch"], 1)
+            single["hbm_bytes_calibrated_per_launch"] = r1 + w1
+            single["read_bytes_calibrated_per_launch"] = r1
+            single["gather_read_bytes_calibrated_per_launch"] = g1
         d["calibration"] = {"source": os.path.relpath(cal_path, ROOT), "stream_read_bytes_per_agent_step": k["stream"],
                             "stream_factor": f_stream, "gather_pattern": k["gather"], "gather_factor": f_g,
                             "model": "reads = stream + (FETCH_raw - f_stream * stream) / f_gather; writes = WRITE_raw"}

@@ -135,8 +135,10 @@ def test_bench_helpers():
     # PMC traffic per episode: the chained figure for chained runs, the one-launch-per-episode one otherwise
     t = bench.load_traffic(os.path.join(bench.ROOT, "profiles", "pmc_traffic.json"),
                            json.load(open(os.path.join(bench.ROOT, "profiles", "pmc_traffic.json")))["workload"])
-    assert bench.traffic_per_episode(t, True) == t["hbm_bytes_per_episode"]
-    assert bench.traffic_per_episode(t, False) == t["one_launch_per_episode"]["hbm_bytes_per_launch"]
+    # (round 6: the counter factors calibrated per access pattern, scripts/recalibrate_traffic.py)
+    assert bench.traffic_per_episode(t, True) == t["hbm_bytes_calibrated_per_episode"]
+    assert bench.traffic_per_episode(t, False) == t["one_launch_per_episode"]["hbm_bytes_calibrated_per_launch"]
+    assert t["hbm_bytes_calibrated_per_episode"] < t["hbm_bytes_per_episode"]  # the uniform x2 overstated reads
     assert bench.traffic_per_episode(None, True) is None
 
 

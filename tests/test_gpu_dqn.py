@@ -80,6 +80,17 @@ def test_train_batch_matches_oracle_step():
         odqn.soft_update(tg_o, th_o, 0.005)
         assert np.float32(loss) == lo[0], (loss, lo[0])
         gm, lm = odqn.gradients(th_m, s[None], a[None], r[None], ns[None], tg_m, 0.95)
+        if k == 0:
+            # the first Adam step's m is (1 - beta1) * g: the device's gradient against the
+            # matmul-order one at north_star's 1e-5 of each parameter group's scale
+            # (tests/test_cpu_dqn_orders.py; the update itself amplifies near-zero components)
+            b1c = np.float64(np.float32(1.0) - np.float32(0.9))
+            g_dev = eng.get_weights("adam_m")[0].astype(np.float64) / b1c
+            g_mm = gm[0].astype(np.float64)
+            g_mm[:320] = np.clip(g_mm[:320], -1.0, 1.0)  # the first kernel's clip (rl.py:329, adam_step)
+            for lo, hi in ((0, 320), (320, 384), (384, 4480), (4480, 4544), (4544, 4608), (4608, 4609)):
+                scale = np.abs(g_mm[lo:hi]).max()
+                assert np.abs(g_dev[lo:hi] - g_mm[lo:hi]).max() <= 1e-5 * scale, (lo, hi)
         odqn.adam_step(th_m, m_m, v_m, gm, k + 1)
         odqn.soft_update(tg_m, th_m, 0.005)
         assert abs(loss - lm[0]) <= 1e-5 * abs(lm[0])

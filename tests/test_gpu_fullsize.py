@@ -177,6 +177,14 @@ def test_full_size_config5_shared_gradient_segments_against_oracle():
         partials, _ = odqn.train_block(th0, th0, b.reshape(bps, APB, 32, 10), 0.95)
         want = odqn.fold_segments(partials, bps)[0]
         assert np.array_equal(segs[g], want), f"segment {g}: max |diff| {np.abs(segs[g] - want).max()}"
+        # independent: the sum of the same agents' matmul-order gradients (rl.py:307-333 as numpy
+        # matmuls), within north_star's 1e-5 of each parameter group's scale (test_cpu_dqn_orders.py)
+        th_n = np.repeat(th0[None], seg_agents, 0)
+        gm, _ = odqn.gradients(th_n, b[..., 0:4], b[..., 4], b[..., 5], b[..., 6:10], th_n, 0.95)
+        gsum = gm.astype(np.float64).sum(0)
+        for lo, hi in ((0, 320), (320, 384), (384, 4480), (4480, 4544), (4544, 4608), (4608, 4609)):
+            err = np.abs(segs[g][lo:hi] - gsum[lo:hi]).max()
+            assert err <= 1e-5 * np.abs(gsum[lo:hi]).max(), (g, lo, hi, err)
     eng.close()
 
 
