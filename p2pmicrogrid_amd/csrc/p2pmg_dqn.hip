@@ -1457,18 +1457,23 @@ hipError_t launch_dqn_sample(const DqnParams& d, hipStream_t st) {
 hipError_t launch_dqn_reduce_adam(const DqnParams& d, int segments, bool adam, hipStream_t st) {
   if (segments < 1 || d.bps < 1 || (adam && segments != 1)) return hipErrorInvalidValue;
   const dim3 grid((kDqnParams + kRedParams - 1) / kRedParams, segments);
-  // the fold: runs of per = ceil(bps / 16) partials, the first 4 or 8 of each run loaded together
-  const bool b4 = (d.bps + kRedSlices - 1) / kRedSlices <= 4;
+  // the fold: runs of per = ceil(bps / 16) partials, the first 4 or 8 of each run loaded together.
+  // fold_spt 0 (auto): 4 runs per thread while a run fits one 8-load batch; longer runs (one segment
+  // per rank at world > 1: 512 partials, runs of 32) keep the reduce kernel's form, whose 1024 threads
+  // each have a whole run of up to 48 loads in flight
+  const int per = (d.bps + kRedSlices - 1) / kRedSlices;
+  const bool b4 = per <= 4;
+  const int spt = d.fold_spt ? d.fold_spt : (per <= 8 ? 4 : 1);
 #define P2PMG_FOLD(SPT)                                                                                           \
   if (b4) hipLaunchKernelGGL((dqn_fold_kernel<SPT, 4>), grid, dim3(kRedParams * kRedSlices / SPT), 0, st, d);   \
   else hipLaunchKernelGGL((dqn_fold_kernel<SPT, 8>), grid, dim3(kRedParams * kRedSlices / SPT), 0, st, d);
-  if (adam || d.fold_spt == 1) {
+  if (adam || spt == 1) {
     hipLaunchKernelGGL(dqn_reduce_adam_kernel, grid, dim3(kRedParams * kRedSlices), 0, st, d, adam ? 1 : 0);
-  } else if (d.fold_spt == 2) {
+  } else if (spt == 2) {
     P2PMG_FOLD(2)
-  } else if (d.fold_spt == 8) {
+  } else if (spt == 8) {
     P2PMG_FOLD(8)
-  } else if (d.fold_spt == 16) {
+  } else if (spt == 16) {
     P2PMG_FOLD(16)
   } else {
     P2PMG_FOLD(4)

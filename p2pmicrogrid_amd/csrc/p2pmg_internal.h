@@ -124,7 +124,7 @@ struct DqnParams {
   float *theta_out, *target_out, *m_out, *v_out;
   int adam_pending;          // 1: this act launch first applies the previous env step's gathered Adam step
   int adam_tpb;              // post-exchange Adam launch: threads per workgroup (256 default; 64, 128)
-  int fold_spt;              // segment fold: runs per thread (4 default; 1 = dqn_reduce_adam_kernel; 2, 8, 16)
+  int fold_spt;              // segment fold: runs per thread (0 auto: 4 for runs <= 8, else 1 = the reduce kernel)
 };
 hipError_t launch_dqn_act(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_sample(const DqnParams& p, hipStream_t stream);

@@ -1717,7 +1717,7 @@ static p2pmg::DqnParams dqn_params(p2pmg_ctx* c, const EpisodeParams& e) {
   d.m_out = d.adam_m;
   d.v_out = d.adam_v;
   d.adam_pending = 0;
-  d.fold_spt = 4;
+  d.fold_spt = 0;  // auto (launch_dqn_reduce_adam)
   d.adam_tpb = 256;
   return d;
 }
@@ -1879,9 +1879,9 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
     d.act_wave = (v && !strcmp(v, "wave")) ? 1 : 0;
     const char* g = getenv("P2PMG_ACT_AGW");  // 8: the 8-slot MFMA act workgroups (tests, A/B)
     d.act_agw = (g && atoi(g) == 8) ? 8 : 16;
-    const char* f = getenv("P2PMG_FOLD_SPT");  // segment fold runs per thread: 1, 2, 4 (default), 8, 16 (A/B)
-    const int fs = f ? atoi(f) : 4;
-    d.fold_spt = (fs == 1 || fs == 2 || fs == 8 || fs == 16) ? fs : 4;
+    const char* f = getenv("P2PMG_FOLD_SPT");  // segment fold runs per thread: 1, 2, 4, 8, 16 (A/B); else auto
+    const int fs = f ? atoi(f) : 0;
+    d.fold_spt = (fs == 1 || fs == 2 || fs == 4 || fs == 8 || fs == 16) ? fs : 0;
     const char* at = getenv("P2PMG_ADAM_TPB");  // post-exchange Adam workgroup size: 64, 128, 256 (default)
     d.adam_tpb = at ? atoi(at) : 256;
   }
