@@ -1815,7 +1815,7 @@ static int dqn_gather_segments(p2pmg_ctx* c) {
 }
 
 // defer (the shared network's split path, act kernel able to fuse it): the post-exchange Adam step is
-// left pending (d.adam_pending) for the next env step's act launch, or dqn_settle after the last step
+// left pending (d.adam_pending) for the next env step's act launch, or the episode loop's settle
 static int dqn_train_step(p2pmg_ctx* c, p2pmg::DqnParams& d, bool same, bool defer) {
   // one env step trains every network once (community.py:158-168); the Adam step counters advance
   // only once every launch of the step is enqueued (a failed exchange leaves weights and counters
