@@ -122,6 +122,41 @@ __global__ __launch_bounds__(kWave) void dqn_sample_kernel(const DqnParams d) {
   sample_slots(d, blockIdx.x, threadIdx.x, d.added[blockIdx.x]);
 }
 
+// ReplayBuffer.sample_batch (rl.py:226-241) of every env step of a Philox training episode in ONE
+// throughput launch ahead of it: thread = (step t, agent a), the 32 draws of
+// oracle/philox.py::sample_draws with Floyd's rule walked in order (draw q takes count - 32 + q when
+// r_q equals an earlier draw's final index), written as deque indices [T][A][32] u16 -- the layout
+// replay mode uploads (p2pmg_dqn_set_samples), which the act kernels read instead of drawing in
+// their latency-bound tail.  Every training env step appends one transition per agent before it
+// samples (agent.py:338-342), so step t's count follows from the episode-start count.
+__global__ __launch_bounds__(256) void dqn_sample_prepass_kernel(const DqnParams d, uint16_t* __restrict__ out) {
+  const EpisodeParams& p = d.e;
+  const size_t A = (size_t)p.A;
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (size_t)p.T * A) return;
+  const int t = (int)(k / A), a = (int)(k % A);
+  const int n_add = d.added[a] + t + 1;
+  const int count = n_add < d.cap ? n_add : d.cap;
+  int idx[kB];
+#pragma unroll
+  for (int q = 0; q < kB; ++q) {
+    uint32_t c0 = (uint32_t)t, c1 = (uint32_t)p.episode, c2 = p.agent_offset + (uint32_t)a, c3 = kTagSample + (uint32_t)q;
+    philox4x32_10(c0, c1, c2, c3, p.seed_lo, p.seed_hi);
+    const int r = (int)__umulhi(c0, (uint32_t)(count - kB + q + 1));
+    bool taken = false;
+#pragma unroll
+    for (int l = 0; l < q; ++l) taken = taken || idx[l] == r;
+    idx[q] = taken ? count - kB + q : r;
+  }
+  uint4* o = reinterpret_cast<uint4*>(out + k * kB);
+#pragma unroll
+  for (int v = 0; v < kB / 8; ++v) {
+    const int* x = idx + 8 * v;
+    o[v] = make_uint4((uint32_t)x[0] | ((uint32_t)x[1] << 16), (uint32_t)x[2] | ((uint32_t)x[3] << 16),
+                      (uint32_t)x[4] | ((uint32_t)x[5] << 16), (uint32_t)x[6] | ((uint32_t)x[7] << 16));
+  }
+}
+
 // ----------------------------------------------------------------- act: one env step
 // dqn_act_kernel<NC, WIDE>: one workgroup per scenario.  WIDE = false: NC = N agents compiled in
 // (N <= 16), one wave per agent.  WIDE = true: any n = p.N <= NC (the community sizes 9..15 and
@@ -1446,6 +1481,13 @@ hipError_t launch_dqn_train(const DqnParams& d, int blocks, bool shared_partials
     hipLaunchKernelGGL(dqn_train_kernel<true>, dim3(blocks), dim3(256), 0, st, d);
   else
     hipLaunchKernelGGL(dqn_train_kernel<false>, dim3(blocks), dim3(256), 0, st, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_dqn_sample_prepass(const DqnParams& d, uint16_t* out, hipStream_t st) {
+  const size_t n = (size_t)d.e.T * (size_t)d.e.A;
+  if (n == 0 || d.cap < kB || d.cap > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dqn_sample_prepass_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, out);
   return hipGetLastError();
 }
 

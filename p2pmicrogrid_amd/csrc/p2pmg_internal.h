@@ -128,6 +128,9 @@ struct DqnParams {
 };
 hipError_t launch_dqn_act(const DqnParams& p, hipStream_t stream);
 hipError_t launch_dqn_sample(const DqnParams& p, hipStream_t stream);
+// every env step's Philox replay draws of the episode p describes, as deque indices [T][A][32] u16
+// (the replay-mode sample layout), from the episode-start counts d.added
+hipError_t launch_dqn_sample_prepass(const DqnParams& p, uint16_t* out, hipStream_t stream);
 hipError_t launch_dqn_train(const DqnParams& p, int blocks, bool shared_partials, hipStream_t stream);
 int dqn_train_blocks_per_cu();  // train workgroups resident per CU (the build's occupancy target)
 // each local segment's sum of its train-workgroup partials -> segs[seg_first + j] (segments = local

@@ -125,6 +125,7 @@ struct p2pmg_ctx {
   float* d_buf = nullptr;     // [A][capacity][10]
   int32_t* d_added = nullptr; // [A]
   uint16_t* d_samples = nullptr;  // [T][A][32]
+  uint16_t* d_samples_px = nullptr;  // [T][A][32]: a Philox training episode's draws (dqn_sample_prepass_kernel)
   bool have_samples = false;
   float* d_ep_acc = nullptr;  // [S]
   float* rec_loss = nullptr;  // [T][A]
@@ -394,6 +395,7 @@ int p2pmg_destroy(p2pmg_ctx* c) {
   dfree(c->d_buf);
   dfree(c->d_added);
   dfree(c->d_samples);
+  dfree(c->d_samples_px);
   dfree(c->d_ep_acc);
   dfree(c->rec_loss);
   if (c->comm && rccl()) rccl()->commDestroy(c->comm);
@@ -1921,6 +1923,19 @@ static int dqn_run_episode(p2pmg_ctx* c, const p2pmg_episode_args* args) {
   };
   const int slot = (int)(c->n_timed % p2pmg_ctx::kRing);
   HIP_TRY(c, hipEventRecord(c->ring[2 * slot], c->stream));
+  // Philox training: every env step's replay draws in one throughput launch ahead of the episode,
+  // read by the act launches like uploaded samples (P2PMG_DQN_SAMPLE_PREPASS=0: drawn in each act
+  // launch's tail, as the episode's first form did)
+  {
+    const char* px_env = getenv("P2PMG_DQN_SAMPLE_PREPASS");
+    const bool no_px = px_env && !strcmp(px_env, "0");
+    const size_t n = (size_t)c->T * c->A * p2pmg::kDqnBatch;
+    if (mode == P2PMG_MODE_TRAIN && args->rng == P2PMG_RNG_PHILOX && !no_px && n <= ((size_t)1 << 30)) {
+      if (!c->d_samples_px) HIP_TRY(c, dmalloc(&c->d_samples_px, n));
+      HIP_TRY(c, p2pmg::launch_dqn_sample_prepass(d, c->d_samples_px, c->stream));
+      d.samples = c->d_samples_px;
+    }
+  }
   for (int t = 0; t < c->T; ++t) {
     d.t = t;
     d.e.mode = mode;

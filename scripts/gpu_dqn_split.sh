@@ -7,15 +7,17 @@
 #   splitfoldK   the fold with K = 2, 8 or 16 runs per thread (P2PMG_FOLD_SPT=K)
 #   splitact     the Adam step inside the next env step's act launch (P2PMG_DQN_ADAM=act)
 #   splitadamK   the standalone Adam launch with K = 64 or 128 threads per workgroup (P2PMG_ADAM_TPB=K)
+#   fusednopx    the fused path with the replay draws in each act launch (P2PMG_DQN_SAMPLE_PREPASS=0)
 # Output under gpurun_out/<tag>/dqn_split/.
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
 O="$R/gpurun_out/${1:-r06}/dqn_split"; mkdir -p "$O"
 FORMS="${2:-fused split splitfold1 splitfold16 splitact}"
 setform() {
-  unset P2PMG_DQN_ADAM P2PMG_FOLD_SPT P2PMG_ADAM_TPB
+  unset P2PMG_DQN_ADAM P2PMG_FOLD_SPT P2PMG_ADAM_TPB P2PMG_DQN_SAMPLE_PREPASS
   A="--grad-segments 8 --rccl-world1"
   case $1 in
     fused) A="" ;;
+    fusednopx) A=""; export P2PMG_DQN_SAMPLE_PREPASS=0 ;;
     splitfold1) export P2PMG_FOLD_SPT=1 ;;
     splitfold*) export P2PMG_FOLD_SPT=${1#splitfold} ;;
     splitact) export P2PMG_DQN_ADAM=act ;;

@@ -229,6 +229,16 @@ def test_split_path_forms_match_oracle(monkeypatch, form, S, N, R, apb, segments
     _episodes_vs_oracle(S, N, R, True, apb, segments)
 
 
+@pytest.mark.parametrize("prepass", ["1", "0"])
+@pytest.mark.parametrize("S,N,R,shared,apb,segments", [(3, 2, 1, False, 0, 1), (8, 2, 1, True, 3, 4)])
+def test_sample_draw_forms_match_oracle(monkeypatch, prepass, S, N, R, shared, apb, segments):
+    """Philox training's replay draws (ReplayBuffer.sample_batch rl.py:226-241, Floyd's rule) from
+    the per-episode pre-pass (dqn_sample_prepass_kernel, default) or drawn in each act launch's tail
+    (P2PMG_DQN_SAMPLE_PREPASS=0): both bit for bit the oracle."""
+    monkeypatch.setenv("P2PMG_DQN_SAMPLE_PREPASS", prepass)
+    _episodes_vs_oracle(S, N, R, shared, apb, segments)
+
+
 @pytest.mark.parametrize("spt", ["4", "2", "8", "16"])
 def test_fold_forms_agree_on_long_runs(monkeypatch, spt):
     """Segments of 130 one-agent train workgroups (runs of 9 partials: the fold's 8-load batch and
