@@ -142,6 +142,22 @@ def test_bench_helpers():
     assert bench.traffic_per_episode(None, True) is None
 
 
+@pytest.mark.parametrize("field,value,status", [
+    ("n_agents", 65, 5), ("n_agents", 0, 1), ("n_scenarios", 0, 1), ("horizon", 0, 1), ("rounds", -1, 1),
+    ("rounds", 4096, 5), ("n_actions", 4, 5), ("q_dtype", 7, 1)])
+def test_create_rejects_out_of_range_configs(field, value, status):
+    """p2pmg_create's bounds (include/p2pmg.h): 1 <= N <= 64 agents, R + 1 <= 4096 rounds, at least
+    one scenario and one step, the reference's 3 actions, f64 / f32 tables.  Checked before any
+    device call, so the errors come back here without a GPU."""
+    import ctypes as C
+    from p2pmicrogrid_amd import _lib
+    cfg = _lib.default_config()
+    setattr(cfg, field, value)
+    ctx = C.c_void_p()
+    assert _lib.lib().p2pmg_create(C.byref(cfg), 0, C.byref(ctx)) == status
+    assert not ctx.value
+
+
 def test_device_count_without_gpu_is_zero_or_more():
     from p2pmicrogrid_amd import _lib
     assert _lib.device_count() >= 0

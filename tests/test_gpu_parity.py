@@ -172,7 +172,9 @@ def test_any_community_size_matches_oracle(N, R, q_dtype):
                                                   (2, 8, "auto", "prepass"), (12, 11, "auto", "inkernel"),
                                                   (5, 12, "tile", "prepass"),
                                                   # tens of rounds: replay words 0..10, Philox blocks 0..10
-                                                  (4, 40, "auto", "inkernel"), (17, 33, "auto", "prepass")])
+                                                  (4, 40, "auto", "inkernel"), (17, 33, "auto", "prepass"),
+                                                  # the bound: R + 1 = 4096 (include/p2pmg.h)
+                                                  (2, 4095, "auto", "inkernel")])
 def test_more_than_eight_rounds_match_oracle(N, R, kernel, placement):
     """R + 1 > 8 negotiation rounds (community.py:75 runs any `rounds`): rounds 8 and up take their
     exploration codes one at a time (replay words 2.. and Philox words k = t (R + 1) + r), in the
