@@ -179,7 +179,7 @@ def test_more_than_eight_rounds_match_oracle(N, R, kernel, placement):
     """R + 1 > 8 negotiation rounds (community.py:75 runs any `rounds`): rounds 8 and up take their
     exploration codes one at a time (replay words 2.. and Philox words k = t (R + 1) + r), in the
     register and tile forms, Philox pre-pass and in-kernel draws, against the oracle."""
-    S, T = 24, 10
+    S, T = (24, 10) if R < 1000 else (4, 4)  # the oracle's per-round loop bounds the 4096-round case
     inp = scenario_batch(S, N, T, seed=29)
     ob = _oracle_for(inp, N, R)
     ob.t_in, ob.t_m = inp.t_in0.copy(), inp.t_m0.copy()
