@@ -495,7 +495,7 @@ def run_dqn(args, rank, world, local, S, N, R, T, steps, warmup, cpu_seconds):
                        "parallelism": f"scenario-sharded x{world}, data-parallel shared network"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": achieved / MFMA_F32_PEAK_TFS, "traffic": None,
-                         "kernel": "DQN episode: T x (dqn_act_kernel + dqn_train_kernel + reduce + adam)",
+                         "kernel": "DQN episode: the replay-draw pre-pass + T x (act + train + reduce + adam)",
                          "kernel_ms": episode_ms, "flop_per_agent_step": flop,
                          "flop_per_episode": flop * steps_per_episode, "timed_launches": int(len(kms))},
             "mean_episode_reward": metrics[0] / metrics[1],
