@@ -235,6 +235,18 @@ def all_gather_float(x: float, world: int):
     return [float(t.item()) for t in out]
 
 
+def agree_setup(err, world: int):
+    """A workload's setup (inputs, context, uploads) went through on every rank, or the workload is
+    dropped on every rank: the ranks exchange one flag over gloo before their first collective, so a
+    rank whose setup failed (device or shared memory) never leaves the others waiting in one."""
+    flags = all_gather_float(0.0 if err is not None else 1.0, world)
+    if err is not None:
+        raise err
+    bad = [r for r, f in enumerate(flags) if f != 1.0]
+    if bad:
+        raise RuntimeError(f"workload setup failed on rank(s) {bad}")
+
+
 def barrier(world):
     if world > 1:
         import torch.distributed as dist
@@ -419,18 +431,27 @@ def run_dqn(args, rank, world, local, S, N, R, T, steps, warmup, cpu_seconds):
     from p2pmicrogrid_amd.dataset import scenario_batch
     t_setup = time.perf_counter()
     first = rank * S
-    inp = scenario_batch(S, N, T, first_scenario=first)
-    dkw = {}
-    if args.grad_segments:  # the split path (segment fold -> exchange -> dqn_adam_shared_kernel) at any world
-        dkw["grad_segments"] = args.grad_segments
-    if args.agents_per_block:
-        dkw["agents_per_block"] = args.agents_per_block
-    eng = dqn_engine_class()(S, N, R, T, shared=True, device=local, scenario_offset=first, init_seed=0, **dkw)
-    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
-    eng.set_profiles(inp.load_w, inp.pv_w)
-    eng.set_max_in(inp.max_in)
-    eng.set_temperatures(inp.t_in0, inp.t_m0)
-    del inp
+
+    def build():
+        inp = scenario_batch(S, N, T, first_scenario=first)
+        dkw = {}
+        if args.grad_segments:  # the split path (segment fold -> exchange -> dqn_adam_shared_kernel) at any world
+            dkw["grad_segments"] = args.grad_segments
+        if args.agents_per_block:
+            dkw["agents_per_block"] = args.agents_per_block
+        e = dqn_engine_class()(S, N, R, T, shared=True, device=local, scenario_offset=first, init_seed=0, **dkw)
+        e.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+        e.set_profiles(inp.load_w, inp.pv_w)
+        e.set_max_in(inp.max_in)
+        e.set_temperatures(inp.t_in0, inp.t_m0)
+        return e
+
+    eng, err = None, None
+    try:
+        eng = build()
+    except Exception as e:  # noqa: BLE001  (agree_setup re-raises it on this rank, and on the others)
+        err = e
+    agree_setup(err, world)
     xk = exchange_kind(args, world)
     fallback, comm_err = None, ""
     if xk != "host":  # gradient-segment all-gather every env step + metrics over RCCL
@@ -736,30 +757,42 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
     S, N, T, q_dtype = S or S0, N or N0, T or T0, q_dtype or qd0
     R = R0 if R is None else R
     first = rank * S
-    mix = asset_mix(S, N, first_scenario=first, battery_j=BATTERY_J) if hetero else None
-    gen = None
-    if S * N * T >= PARALLEL_GEN_ELEMS and not os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
-        # configs[3]'s year of profiles (9.2 GB per GPU): generator blocks on the host cores, into shared memory
-        gen = SharedScenarioInputs(S, N, T, cpu_workers()[0], first_scenario=first, mix=mix)
-        inp = gen.inputs
-    else:
-        inp = scenario_batch(S, N, T, first_scenario=first)
-        if hetero:
-            inp = apply_asset_mix(inp, mix)
-    t_gen = time.perf_counter() - t_setup
-    eng = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=local, scenario_offset=first, shared_q=shared)
-    eng.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
-    eng.set_profiles(inp.load_w, inp.pv_w)
-    eng.set_max_in(inp.max_in)
-    eng.set_temperatures(inp.t_in0, inp.t_m0)
-    del inp
-    if gen is not None:
-        gen.close()
-    if mix is not None:
-        eng.set_hp_levels(mix.hp_levels)
-        eng.set_battery(mix.battery_capacity)
-    elif battery:
-        eng.set_battery(BATTERY_J)
+
+    def build():
+        mix = asset_mix(S, N, first_scenario=first, battery_j=BATTERY_J) if hetero else None
+        gen = None
+        if S * N * T >= PARALLEL_GEN_ELEMS and not os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
+            # configs[3]'s year of profiles (9.2 GB per GPU): generator blocks on the host cores, into shared memory
+            gen = SharedScenarioInputs(S, N, T, cpu_workers()[0], first_scenario=first, mix=mix)
+            inp = gen.inputs
+        else:
+            inp = scenario_batch(S, N, T, first_scenario=first)
+            if hetero:
+                inp = apply_asset_mix(inp, mix)
+        tg = time.perf_counter() - t_setup
+        try:
+            e = DeviceCommunityBatch(S, N, R, T, q_dtype=q_dtype, device=local, scenario_offset=first, shared_q=shared)
+            e.set_env(np.broadcast_to(inp.time, inp.t_out.shape), inp.t_out)
+            e.set_profiles(inp.load_w, inp.pv_w)
+            e.set_max_in(inp.max_in)
+            e.set_temperatures(inp.t_in0, inp.t_m0)
+        finally:
+            del inp
+            if gen is not None:
+                gen.close()
+        if mix is not None:
+            e.set_hp_levels(mix.hp_levels)
+            e.set_battery(mix.battery_capacity)
+        elif battery:
+            e.set_battery(BATTERY_J)
+        return e, tg, gen is not None
+
+    eng, t_gen, parallel_gen, err = None, 0.0, False, None
+    try:
+        eng, t_gen, parallel_gen = build()
+    except Exception as e:  # noqa: BLE001  (agree_setup re-raises it on this rank, and on the others)
+        err = e
+    agree_setup(err, world)
     # episode metrics (+ the shared table's per-episode delta all-reduce, which needs RCCL)
     xk = exchange_kind(args, world)
     fallback = None
@@ -954,7 +987,7 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
             # outside the timed region: host input generation (parallel above PARALLEL_GEN_ELEMS) and the
             # context build + upload + zeroed tables
             "setup_s": {"inputs": t_gen, "context_and_upload": t_upload,
-                        "input_generation": "parallel (dataset.SharedScenarioInputs)" if gen is not None else "serial"},
+                        "input_generation": "parallel (dataset.SharedScenarioInputs)" if parallel_gen else "serial"},
         }
         if os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
             out["test_engine"] = os.environ["P2PMG_BENCH_TEST_ENGINE"]

@@ -66,6 +66,10 @@ class BenchOracleDQNEngine:
 
     def __init__(self, S, N, R, T, shared=True, device=0, scenario_offset=0, init_seed=0, seed=42, grad_segments=1,
                  agents_per_block=0):
+        import os
+        fail = os.environ.get("P2PMG_BENCH_TEST_FAIL_DQN_RANK")  # a setup failure on one rank (bench.agree_setup)
+        if fail is not None and os.environ.get("RANK", "0") == fail:
+            raise MemoryError("test: DQN context setup failed on this rank")
         from oracle_engine import OracleDQNEngine
         self._e = OracleDQNEngine(Shard(0, 1, scenario_offset, S), S, N, R, T, "f32", device, seed,
                                   grad_segments=grad_segments, agents_per_block=agents_per_block)

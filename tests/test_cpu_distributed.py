@@ -349,6 +349,19 @@ def _default_line(world, scen_per_rank):
                        *SMALL_DEFAULT_LINE)
 
 
+@pytest.mark.timeout(300)
+def test_bench_setup_failure_on_one_rank_drops_the_workload_everywhere():
+    """configs[4]'s context fails to set up on rank 1 only (P2PMG_BENCH_TEST_FAIL_DQN_RANK): every rank
+    learns it before the workload's first collective (bench.agree_setup), the record carries the
+    error, and the ranks go on to the next record instead of waiting for rank 1 in a collective."""
+    root, env = _bench_env(P2PMG_BENCH_TEST_DQN_ENGINE="bench_test_engine:BenchOracleDQNEngine",
+                           P2PMG_BENCH_TEST_FAIL_DQN_RANK="1")
+    d = _bench_line(root, env, "--gpus", "2", "--scenarios", "4", "--secondary-scenarios", "4",
+                    "--extra-scenarios", "4", *SMALL_DEFAULT_LINE)
+    assert "error" in d["secondary_dqn"] and "rank(s) [1]" in d["secondary_dqn"]["error"]
+    assert d["secondary_year"]["value"] > 0 and d["value"] > 0
+
+
 @pytest.fixture(scope="module")
 def default_line_world1():
     return _default_line(1, 8)
