@@ -763,7 +763,8 @@ def run_tabular(args, rank, world, local, wl, *, S=None, N=None, R=None, T=None,
         gen = None
         if S * N * T >= PARALLEL_GEN_ELEMS and not os.environ.get("P2PMG_BENCH_TEST_ENGINE"):
             # configs[3]'s year of profiles (9.2 GB per GPU): generator blocks on the host cores, into shared memory
-            gen = SharedScenarioInputs(S, N, T, cpu_workers()[0], first_scenario=first, mix=mix)
+            # (at most 16 generator processes per rank: 8 ranks of a node stay within a few hundred)
+            gen = SharedScenarioInputs(S, N, T, min(16, cpu_workers()[0]), first_scenario=first, mix=mix)
             inp = gen.inputs
         else:
             inp = scenario_batch(S, N, T, first_scenario=first)
